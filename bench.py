@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: QP solves/s of the fused HIP convex-MPC solver (BASELINE.json metric).
+
+One "step" = one pass of the hot path (ConvexMPCLocomotion::solveDenseMPC -> solve_mpc:
+condensation + friction-cone QP + force scatter) over one batch of synthetic instances that are
+already resident in HBM. Default workload = BASELINE config 3: batch 65536, horizon 10, fused
+condensation + QP, one GPU. With N GPUs (torchrun, one process per GPU) every rank solves its
+own 65536-instance shard (independent instances, no collective on the data path: weak scaling);
+the step time is the max over ranks.
+
+  python bench.py [--gpus N --steps K --warmup W] [--batch B --horizon H] [--no-cpu-baseline]
+
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "QP solves/sec (N=10, 13-state, 12-force) at batch=65536; 1/2/4/8 GPU"
+FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 dense (VALU = f32 MFMA rate), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def algorithmic_flops(N: int) -> float:
+    """F(N) = F_cond + F_chol (dense, reference algorithm)."""
+    n = 12 * N
+    f_cond = 4056 * (N - 1) + 338 * N + 3900 * N * (N + 1) * (N + 2) / 6 + 312 * N * (N + 1) / 2
+    f_chol = n ** 3 / 3 + 2 * n ** 2
+    return f_cond + f_chol
+
+
+def algorithmic_bytes(N: int) -> int:
+    """compulsory HBM bytes per QP (fp32 record in, forces out)."""
+    return 64 + 48 + 48 * N + 4 * N + 4 + 48 * N
+
+
+def cpu_baseline(prm, N: int, seed: int):
+    """Reference pipeline (fp32 dense-S condensation restated from SolverMPC.cpp + the
+    reference's qpOASES 3.2.0 built from its sources) on host cores, bounded sample."""
+    try:
+        from oracle import oracle as orc
+    except Exception:
+        return None
+    if not orc.ref_available():
+        return None
+    cm = importlib.import_module("quad-periodic-mpc_amd")
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(16, threads))
+    sample = 8192
+    recs = cm.make_instances(sample, N, seed=seed)
+    orc.ref_solve_batch(recs[:64], prm, nthreads=threads)  # warm
+    t0 = time.perf_counter()
+    orc.ref_solve_batch(recs, prm, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": sample / dt, "unit": "QP solves/s", "cores": threads, "kind": "reference",
+            "sample": f"{sample} instances of the same synthetic workload (N={N}), solve_mpc "
+                      f"equivalent per instance: fp32 dense-S condensation (SolverMPC.cpp:566-950 "
+                      f"restated, oracle/cmpc_oracle.c) + reference qpOASES 3.2.0 (setToMPC, "
+                      f"nWSR=100) built from /root/reference; {threads} std::threads; "
+                      f"{dt:.2f} s wall"}
+
+
+def load_traffic(path: str, N: int, batch: int):
+    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC summary."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("horizon") == N and d.get("batch") == batch:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
+    ap.add_argument("--horizon", type=int, default=10)
+    ap.add_argument("--random-contact-frac", type=float, default=0.25)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = tdist
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    cm = importlib.import_module("quad-periodic-mpc_amd")
+    solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+    N, B = args.horizon, args.batch
+    prm = cm.make_params(N)
+    seed = 20251015 + 7919 * rank
+    recs_np = cm.make_instances(B, N, seed=seed, random_contact_frac=args.random_contact_frac)
+    recs = torch.from_numpy(recs_np).to(dev)
+    forces = torch.empty((B, 12 * N), dtype=torch.float32, device=dev)
+    status = torch.empty(B, dtype=torch.uint8, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    solver = solver_mod.BatchSolver(prm, max_batch=B)
+    stream = torch.cuda.ExternalStream(solver.stream_handle, device=dev)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        solver.solve(recs, forces, status, iters)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    if (st != 0).any():
+        print(f"[rank {rank}] WARNING: status counts {np.bincount(st)}", file=sys.stderr)
+
+    # timed region: K steps, bracketed by barrier + synchronize
+    solver.enable_timing(args.steps)
+    barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        solver.solve(recs, forces, status, iters)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    launch_ms, ovf = solver.read_timing()
+    elapsed = max(wall, gpu_ms / 1e3)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    total = B * world * args.steps
+    value = total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    # dominant kernel: the 64-lane size class (every instance with <= 64 stance force variables)
+    c1 = launch_ms[:, 0] if launch_ms.size else np.array([np.nan])
+    c2 = launch_ms[:, 1] if launch_ms.size else np.array([np.nan])
+    units1 = B - ovf
+    t1 = float(np.mean(c1)) * 1e-3
+    fl = algorithmic_flops(N)
+    achieved = fl * units1 / t1 / 1e12 if t1 > 0 else None
+    traffic = load_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), N, B)
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(prm, N, seed)
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "QP solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"BASELINE config 3: fused condensation + friction-cone QP, horizon N={N}, "
+                        f"batch={B} per GPU (A1 trot at random phase + "
+                        f"{int(args.random_contact_frac * 100)}% Bernoulli(0.5) contacts), "
+                        f"inputs resident in HBM",
+            "global_batch": B * world,
+            "batch_per_gpu": B,
+            "horizon": N,
+            "parallelism": f"dp{world} (independent instance shards, no data-path collective)",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "achieved": round(achieved, 3) if achieved else None,
+            "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 5) if achieved else None,
+            "traffic": traffic,
+            "kernel": "cmpc_solve_kernel<1> (64-lane class)",
+            "units_per_launch": int(units1),
+            "flops_per_unit": fl,
+            "avg_launch_ms": round(float(np.mean(c1)), 4),
+            "class2_avg_launch_ms": round(float(np.mean(c2)), 4),
+            "class2_units_per_launch": int(ovf),
+            "note": "FP32 compute roof (f32 VALU = f32 MFMA peak); algorithmic FLOPs per SURVEY "
+                    "§8(d) F(N) (dense reference algorithm); HBM bytes/QP "
+                    f"{algorithmic_bytes(N)} -> {algorithmic_bytes(N) * value / 1e9:.2f} GB/s",
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

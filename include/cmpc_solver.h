@@ -1,0 +1,141 @@
+/*
+ * cmpc_solver.h — C ABI of the MI355X-native batched convex-MPC solver (libcmpc_hip.so).
+ *
+ * Two surfaces live here:
+ *
+ *  1. The reference's single-instance SolverMPC interface, unchanged, so the be2r_cmpc_unitree
+ *     FSM links against this library instead of SolverMPC.cpp + convexMPC_interface.cpp +
+ *     RobotState.cpp (reference: be2r_cmpc_unitree/src/controllers/convexMPC/convexMPC_interface.h:44-52).
+ *     Same names, same argument meaning, same call protocol
+ *       setup_problem -> update_x_drag -> update_solver_settings -> update_problem_data_floats
+ *       -> get_solution(0..11)
+ *     (ConvexMPCLocomotion.cpp:807-836). The solve runs on the GPU through the batched path with
+ *     batch = 1.
+ *
+ *  2. A new reentrant batched API (cmpc_batch_*): one handle per stream, a batch of independent
+ *     MPC instances packed as fixed-stride fp32 records (layout below), forces + status out.
+ *
+ * No torch types cross this boundary: plain pointers and sizes only.
+ */
+#ifndef CMPC_SOLVER_H
+#define CMPC_SOLVER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+#define CMPC_EXTERNC extern "C"
+#else
+#define CMPC_EXTERNC
+#endif
+
+/* ------------------------------------------------------------------------------------------ */
+/* Instance record layout (fp32 words).                                                       */
+/* One record = one solve_mpc() call's per-instance data (SolverMPC.cpp:566-655).             */
+/* ------------------------------------------------------------------------------------------ */
+#define CMPC_REC_P        0   /* p[3]      body position (world)          update_data_t.p      */
+#define CMPC_REC_V        3   /* v[3]      body velocity (world)          update_data_t.v      */
+#define CMPC_REC_Q        6   /* q[4]      orientation quaternion w,x,y,z update_data_t.q      */
+#define CMPC_REC_W        10  /* w[3]      angular velocity (world)       update_data_t.w      */
+#define CMPC_REC_R        13  /* r[12]     foot offsets, axis-major 3x4:  r[axis*4 + leg]      */
+#define CMPC_REC_RPY      25  /* roll, pitch, yaw (stored, unused by the solve, as reference)  */
+#define CMPC_REC_XDRAG    28  /* x_drag    A(11,9) coefficient            update_x_drag()      */
+#define CMPC_REC_FEST3    29  /* f_est(3): compensation force fed into qg (config 5)           */
+#define CMPC_REC_FLAGS    30  /* bit-cast uint32: bit0 = use f_est in qg (history > 500)       */
+#define CMPC_REC_HDR      32  /* header words; traj follows                                    */
+/* traj[12*N] fp32 at CMPC_REC_HDR, then gait[4*N] uint8 (step-major, leg-minor) packed into
+ * N words, then padding to a 16-byte multiple. */
+#define CMPC_REC_TRAJ(N)   (CMPC_REC_HDR)
+#define CMPC_REC_GAIT(N)   (CMPC_REC_HDR + 12 * (N))
+#define CMPC_REC_WORDS(N)  ((CMPC_REC_HDR + 13 * (N) + 3) & ~3)
+
+#define CMPC_MAX_HORIZON  24  /* reference caps at 19 (SolverMPC.cpp:113-116); lifted for N=20 */
+
+/* Per-instance status (batched API). The reference has no status: on qpOASES failure it prints
+ * "failed to solve!" and leaves stale forces (SolverMPC.cpp:964-968). Documented deviation:
+ * forces are zero when status != CMPC_OK. */
+enum {
+  CMPC_OK = 0,
+  CMPC_MAX_ITER = 1,      /* active-set iteration cap (reference nWSR = 100) reached          */
+  CMPC_INFEASIBLE = 2,    /* friction-pyramid QP infeasible                                    */
+  CMPC_NOT_PD = 3,        /* Hessian factorisation failed                                      */
+  CMPC_BAD_INPUT = 4      /* horizon out of range / non-finite input                           */
+};
+
+/* Batch-shared problem parameters (problem_setup + the update_data_t scalars that the caller
+ * keeps constant across instances: ConvexMPCLocomotion.cpp:617,623,807). */
+typedef struct cmpc_params {
+  float dt;           /* dtMPC (s)                                                              */
+  float mu;           /* friction coefficient; fmat uses 1/mu (SolverMPC.cpp:657-660)           */
+  float f_max;        /* ub(fz) = gait * f_max                                                  */
+  int   horizon;      /* N, 1..CMPC_MAX_HORIZON                                                 */
+  float weights[12];  /* diagonal state weights (13th = 0)                                      */
+  float alpha;        /* force regularisation: qH = 2(B'SB + alpha I)                          */
+  int   max_iter;     /* active-set iteration cap (reference: nWSR = 100)                       */
+} cmpc_params;
+
+typedef struct cmpc_batch cmpc_batch;
+
+/* ------------------------------------------------------------------------------------------ */
+/* 1. Reference single-instance interface (convexMPC_interface.h:44-52)                       */
+/* ------------------------------------------------------------------------------------------ */
+/* Replaces convexMPC_interface.cpp:44-67 (+ resize_qp_mats, SolverMPC.cpp:149-250). */
+CMPC_EXTERNC void setup_problem(double dt, int horizon, double mu, double f_max);
+/* Replaces convexMPC_interface.cpp:96-107 (double-precision variant, yaw only). */
+CMPC_EXTERNC void update_problem_data(double* p, double* v, double* q, double* w, double* r,
+                                      double yaw, double* weights, double* state_trajectory,
+                                      double alpha, int* gait);
+/* Replaces convexMPC_interface.cpp:156-162: q_soln[index], 0 before the first solve. */
+CMPC_EXTERNC double get_solution(int index);
+/* Replaces convexMPC_interface.cpp:109-130 (use_jcqp thresholds >1.5 -> 2, >0.5 -> 1). */
+CMPC_EXTERNC void update_solver_settings(int max_iter, double rho, double sigma,
+                                         double solver_alpha, double terminate, double use_jcqp);
+/* Replaces convexMPC_interface.cpp:132-149 -> solve_mpc (SolverMPC.cpp:566-1089). */
+CMPC_EXTERNC void update_problem_data_floats(float* p, float* v, float* q, float* w, float* r,
+                                             float roll, float pitch, float yaw, float* weights,
+                                             float* state_trajectory, float alpha, int* gait);
+#ifdef __cplusplus
+/* C++ linkage, as the reference (convexMPC_interface.h:52; symbol _Z13update_x_dragf). */
+void update_x_drag(float x_drag);
+#endif
+
+/* Globals the reference solver reads but its caller defines (ConvexMPCLocomotion.cpp:610,
+ * be2r_cmpc_unitree_node.cpp:6). Weak definitions in the library; the host program's strong
+ * definitions take precedence. f_ext has Eigen::Matrix<float,6,1> layout (6 floats). */
+CMPC_EXTERNC float f_ext[6];
+CMPC_EXTERNC float simulation_time;
+
+/* ------------------------------------------------------------------------------------------ */
+/* 2. Batched, reentrant API                                                                   */
+/* ------------------------------------------------------------------------------------------ */
+CMPC_EXTERNC int cmpc_record_words(int horizon);
+/* Create a handle bound to the current HIP device; stream may be NULL (a private stream is
+ * created). Scratch for max_batch instances is allocated here, never inside solve. */
+CMPC_EXTERNC int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int max_batch,
+                                   void* hip_stream);
+CMPC_EXTERNC int cmpc_batch_set_params(cmpc_batch* h, const cmpc_params* prm);
+CMPC_EXTERNC void cmpc_batch_destroy(cmpc_batch* h);
+/* Device-resident solve: d_records [batch * cmpc_record_words(N)] fp32, d_forces
+ * [batch * 12N] fp32 (step-major, leg*3+axis), d_status [batch] uint8, d_iters [batch] int32
+ * (may be NULL). Asynchronous on the handle's stream. Returns 0 or a negative error. */
+CMPC_EXTERNC int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int batch,
+                                  float* d_forces, uint8_t* d_status, int32_t* d_iters);
+/* Same, host buffers in and out (H2D + solve + D2H on the handle's stream, synchronous). */
+CMPC_EXTERNC int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int batch,
+                                       float* forces, uint8_t* status, int32_t* iters);
+/* Parity hook for the condensation rows (SolverMPC.cpp:96-146, 806-814): full 12N x 12N qH
+ * (row-major) and qg per instance, all variables kept (no swing elimination). */
+CMPC_EXTERNC int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int batch,
+                                     float* d_H, float* d_g);
+/* Measurement hooks: record HIP events around each size-class launch of the next `steps`
+ * solves; read back per-launch ms pairs [class1, class2] and class 1's overflow count (the
+ * number of instances handed to the 2-wave class in the last solve). Synchronises. */
+CMPC_EXTERNC int cmpc_batch_enable_timing(cmpc_batch* h, int steps);
+CMPC_EXTERNC int cmpc_batch_read_timing(cmpc_batch* h, float* ms, int* steps_recorded,
+                                        int* class1_overflow);
+/* Stream the handle runs on (hipStream_t). */
+CMPC_EXTERNC void* cmpc_batch_stream(cmpc_batch* h);
+/* Last HIP error string for this thread (diagnostics). */
+CMPC_EXTERNC const char* cmpc_last_error(void);
+
+#endif /* CMPC_SOLVER_H */

@@ -1,0 +1,380 @@
+/*
+ * TEST INFRASTRUCTURE ONLY (see cmpc_oracle.h). Reference-faithful CPU restatement of
+ * SolverMPC.cpp:566-982 for one MPC instance. Every function cites the reference lines it
+ * restates. fp32 (Eigen `fpt = float`, common_types.h:14) wherever the reference is fp32; the
+ * reduced QP is double as qpOASES `real_t` (Types.hpp:171).
+ */
+#include "cmpc_oracle.h"
+
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define BIG_NUMBER 5e10f /* SolverMPC.cpp:19 */
+
+/* ---------------------------------------------------------------------------------------- */
+/* small dense helpers (row-major)                                                           */
+/* ---------------------------------------------------------------------------------------- */
+
+/* C[m x n] = A[m x k] * B[k x n], fp32 accumulate, C zeroed first. */
+static void sgemm_nn(int m, int n, int k, const float* A, const float* B, float* C) {
+  memset(C, 0, sizeof(float) * (size_t)m * n);
+  for (int i = 0; i < m; i++) {
+    float* c = C + (size_t)i * n;
+    for (int p = 0; p < k; p++) {
+      const float a = A[(size_t)i * k + p];
+      const float* b = B + (size_t)p * n;
+      for (int j = 0; j < n; j++) c[j] += a * b[j];
+    }
+  }
+}
+
+/* C[m x n] = alpha * A^T * B, A stored [k x m], B [k x n]. */
+static void sgemm_tn(int m, int n, int k, float alpha, const float* A, const float* B, float* C) {
+  memset(C, 0, sizeof(float) * (size_t)m * n);
+  for (int p = 0; p < k; p++) {
+    const float* b = B + (size_t)p * n;
+    for (int i = 0; i < m; i++) {
+      const float a = alpha * A[(size_t)p * m + i];
+      float* c = C + (size_t)i * n;
+      for (int j = 0; j < n; j++) c[j] += a * b[j];
+    }
+  }
+}
+
+/* y[m] = A[m x n] x[n] */
+static void sgemv(int m, int n, const float* A, const float* x, float* y) {
+  for (int i = 0; i < m; i++) {
+    float s = 0.f;
+    for (int j = 0; j < n; j++) s += A[(size_t)i * n + j] * x[j];
+    y[i] = s;
+  }
+}
+
+static void dmm(int m, int n, int k, const double* A, const double* B, double* C) {
+  for (int i = 0; i < m; i++)
+    for (int j = 0; j < n; j++) {
+      double s = 0.0;
+      for (int p = 0; p < k; p++) s += A[i * k + p] * B[p * n + j];
+      C[i * n + j] = s;
+    }
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* RobotState::set (RobotState.cpp:9-50) + quat_to_rpy (SolverMPC.cpp:352-361)               */
+/* ---------------------------------------------------------------------------------------- */
+
+/* Eigen Quaternion::toRotationMatrix (w,x,y,z), no normalisation (RobotState.cpp:36, TODO at :49). */
+static void quat_to_R(const float* q, float R[9]) {
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  const float tx = 2.f * x, ty = 2.f * y, tz = 2.f * z;
+  const float twx = tx * w, twy = ty * w, twz = tz * w;
+  const float txx = tx * x, txy = ty * x, txz = tz * x;
+  const float tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  R[0] = 1.f - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
+  R[3] = txy + twz;         R[4] = 1.f - (txx + tzz); R[5] = tyz - twx;
+  R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.f - (txx + tyy);
+}
+
+static void quat_to_rpy(const float* q, float rpy[3]) {
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  /* t_min(-2.*(...), .99999): double arithmetic, upper clamp only, stored as fpt */
+  double asd = -2. * (double)(x * z - w * y);
+  if (!(asd < .99999)) asd = .99999;
+  const float as = (float)asd;
+  rpy[0] = (float)atan2((double)(2.f * (x * y + w * z)), (double)(w * w + x * x - y * y - z * z));
+  rpy[1] = (float)asin((double)as);
+  rpy[2] = (float)atan2((double)(2.f * (y * z + w * x)), (double)(w * w - x * x - y * y + z * z));
+}
+
+/* Eigen 3x3 inverse via the adjugate (SolverMPC.cpp:273). */
+static void inv3(const float* m, float* o) {
+  const float c00 = m[4] * m[8] - m[5] * m[7];
+  const float c10 = m[5] * m[6] - m[3] * m[8];
+  const float c20 = m[3] * m[7] - m[4] * m[6];
+  const float det = m[0] * c00 + m[1] * c10 + m[2] * c20;
+  const float id = 1.f / det;
+  o[0] = c00 * id; o[1] = (m[2] * m[7] - m[1] * m[8]) * id; o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+  o[3] = c10 * id; o[4] = (m[0] * m[8] - m[2] * m[6]) * id; o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+  o[6] = c20 * id; o[7] = (m[1] * m[6] - m[0] * m[7]) * id; o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* ct_ss_mats (SolverMPC.cpp:260-279) + Q_ct (:607-615)                                      */
+/* ---------------------------------------------------------------------------------------- */
+static void ct_ss_mats(const float* I_world, float m, const float* r_feet /*3x4*/, const float* R_yaw,
+                       float x_drag, float* A /*13x13*/, float* B /*13x12*/) {
+  memset(A, 0, sizeof(float) * 169);
+  A[3 * 13 + 9] = 1.f;
+  A[11 * 13 + 9] = x_drag;
+  A[4 * 13 + 10] = 1.f;
+  A[5 * 13 + 11] = 1.f;
+  A[11 * 13 + 12] = 1.f;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) A[i * 13 + 6 + j] = R_yaw[j * 3 + i]; /* R_yaw^T */
+
+  memset(B, 0, sizeof(float) * 156);
+  float I_inv[9];
+  inv3(I_world, I_inv);
+  for (int b = 0; b < 4; b++) {
+    const float r0 = r_feet[0 * 4 + b], r1 = r_feet[1 * 4 + b], r2 = r_feet[2 * 4 + b];
+    const float cm[9] = {0.f, -r2, r1, r2, 0.f, -r0, -r1, r0, 0.f};
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        float s = 0.f;
+        for (int k = 0; k < 3; k++) s += I_inv[i * 3 + k] * cm[k * 3 + j];
+        B[(6 + i) * 12 + b * 3 + j] = s;
+      }
+    for (int i = 0; i < 3; i++) B[(9 + i) * 12 + b * 3 + i] = 1.f / m;
+  }
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* c2qp discretisation (SolverMPC.cpp:96-107). expm(dt*[A B Q; 0]) of the 31x31 generator.  */
+/* A^3 = 0 for this A, so M^4 = 0 and the exponential is the finite series                  */
+/* I + M + M^2/2 + M^3/6 — what Eigen's Pade approximant returns up to rounding (a [p/p]      */
+/* Pade of exp matches the Taylor series through order 2p >= 6). Evaluated in double,        */
+/* rounded to fp32.                                                                           */
+/* ---------------------------------------------------------------------------------------- */
+static void discretise(const float* Af, const float* Bf, float dt, float* Adt, float* Bdt, float* Qdt) {
+  double A[169], BQ[13 * 18], A2[169], ABQ[13 * 18], A2BQ[13 * 18];
+  for (int i = 0; i < 169; i++) A[i] = Af[i];
+  for (int i = 0; i < 13; i++) {
+    for (int j = 0; j < 12; j++) BQ[i * 18 + j] = Bf[i * 12 + j];
+    for (int j = 0; j < 6; j++) BQ[i * 18 + 12 + j] = (i >= 6 && i < 12 && (i - 6) == j) ? 1.0 : 0.0;
+  }
+  dmm(13, 13, 13, A, A, A2);
+  dmm(13, 18, 13, A, BQ, ABQ);
+  dmm(13, 18, 13, A, ABQ, A2BQ);
+  const double h = dt, h2 = h * h / 2.0, h3 = h * h * h / 6.0;
+  for (int i = 0; i < 13; i++) {
+    for (int j = 0; j < 13; j++) Adt[i * 13 + j] = (float)((i == j ? 1.0 : 0.0) + h * A[i * 13 + j] + h2 * A2[i * 13 + j]);
+    for (int j = 0; j < 18; j++) {
+      const float v = (float)(h * BQ[i * 18 + j] + h2 * ABQ[i * 18 + j] + h3 * A2BQ[i * 18 + j]);
+      if (j < 12) Bdt[i * 12 + j] = v; else Qdt[i * 6 + (j - 12)] = v;
+    }
+  }
+}
+
+static inline uint8_t rec_gait(const float* rec, int N, int idx) {
+  const uint8_t* g = (const uint8_t*)(rec + CMPC_REC_GAIT(N));
+  return g[idx];
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* solve_mpc up to qH/qg (SolverMPC.cpp:566-814)                                             */
+/* ---------------------------------------------------------------------------------------- */
+size_t oracle_condense_ws_bytes(int N) {
+  const size_t nx = 13u * N, nu = 12u * N;
+  return sizeof(float) * (169u * (N + 1) + nx * 13 + nx * nu + nx * 6 + nx * nx + nu * nx + 2 * nx);
+}
+
+int oracle_condense(const float* rec, const cmpc_params* prm, oracle_cond* out) {
+  const int N = prm->horizon;
+  if (N < 1 || N > CMPC_MAX_HORIZON) return CMPC_BAD_INPUT;
+  void* ws = malloc(oracle_condense_ws_bytes(N));
+  const int st = oracle_condense_ws(rec, prm, out, ws);
+  free(ws);
+  return st;
+}
+
+int oracle_condense_ws(const float* rec, const cmpc_params* prm, oracle_cond* out, void* ws) {
+  const int N = prm->horizon;
+  if (N < 1 || N > CMPC_MAX_HORIZON) return CMPC_BAD_INPUT;
+  const int nx = 13 * N, nu = 12 * N;
+
+  /* RobotState::set */
+  const float* p = rec + CMPC_REC_P;
+  const float* v = rec + CMPC_REC_V;
+  const float* q = rec + CMPC_REC_Q;
+  const float* w = rec + CMPC_REC_W;
+  const float* r = rec + CMPC_REC_R; /* r_feet(rs, c) = r[rs*4 + c] (RobotState.cpp:28-34) */
+  float R[9];
+  quat_to_R(q, R);                   /* R_yaw = R (RobotState.cpp:44) */
+  const float Ibody[3] = {.07f, 0.26f, 0.242f};
+  const float m = 12.0f;             /* RobotState.h:26 */
+
+  float rpy[3];
+  quat_to_rpy(q, rpy);
+  float x0[13] = {rpy[2], rpy[1], rpy[0], p[0], p[1], p[2], w[0], w[1], w[2], v[0], v[1], v[2], -9.8f};
+
+  /* I_world = R_yaw * I_body * R_yaw^T (SolverMPC.cpp:593) */
+  float RI[9], Iw[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) RI[i * 3 + j] = R[i * 3 + j] * Ibody[j];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      float s = 0.f;
+      for (int k = 0; k < 3; k++) s += RI[i * 3 + k] * R[j * 3 + k];
+      Iw[i * 3 + j] = s;
+    }
+
+  float Act[169], Bct[156];
+  ct_ss_mats(Iw, m, r, R, rec[CMPC_REC_XDRAG], Act, Bct);
+
+  float Adt[169], Bdt[156], Qdt[78];
+  discretise(Act, Bct, prm->dt, Adt, Bdt, Qdt);
+
+  /* powerMats, A_qp, B_qp, Q_qp (SolverMPC.cpp:118-139); the N <= 19 cap is lifted. */
+  /* resize_qp_mats zeroes every matrix on every call (SolverMPC.cpp:188-196) */
+  float* pw = (float*)ws;
+  float* Aqp = pw + 169 * (N + 1);
+  float* Bqp = Aqp + nx * 13;
+  float* Qqp = Bqp + (size_t)nx * nu;
+  float* S = Qqp + nx * 6;
+  float* T = S + (size_t)nx * nx;
+  float* vec = T + (size_t)nu * nx;
+  float* tmp = vec + nx;
+  memset(ws, 0, oracle_condense_ws_bytes(N));
+  float blk[13 * 12], qb[13 * 6];
+  memset(pw, 0, sizeof(float) * 169);
+  for (int i = 0; i < 13; i++) pw[i * 14] = 1.f;
+  for (int k = 1; k <= N; k++) sgemm_nn(13, 13, 13, Adt, pw + 169 * (k - 1), pw + 169 * k);
+  for (int rr = 0; rr < N; rr++) {
+    for (int i = 0; i < 13; i++)
+      for (int j = 0; j < 13; j++) Aqp[(13 * rr + i) * 13 + j] = pw[169 * (rr + 1) + i * 13 + j];
+    for (int c = 0; c <= rr; c++) {
+      sgemm_nn(13, 12, 13, pw + 169 * (rr - c), Bdt, blk);
+      sgemm_nn(13, 6, 13, pw + 169 * (rr - c), Qdt, qb);
+      for (int i = 0; i < 13; i++) {
+        for (int j = 0; j < 12; j++) Bqp[(size_t)(13 * rr + i) * nu + 12 * c + j] = blk[i * 12 + j];
+        for (int j = 0; j < 6; j++) Qqp[(13 * rr + i) * 6 + j] += qb[i * 6 + j];
+      }
+    }
+  }
+
+  /* S = diag([weights, 0] x N), dense (SolverMPC.cpp:624-630); X_d (:633-639) */
+  for (int k = 0; k < N; k++)
+    for (int i = 0; i < 12; i++) S[(size_t)(13 * k + i) * nx + 13 * k + i] = prm->weights[i];
+  const float* traj = rec + CMPC_REC_TRAJ(N);
+
+  /* qH = 2 (B^T S B + alpha I) (SolverMPC.cpp:806): (B^T S) B, as Eigen evaluates it. */
+  if (out && out->qH) {
+    sgemm_tn(nu, nx, nx, 1.f, Bqp, S, T);
+    sgemm_nn(nu, nu, nx, T, Bqp, out->qH);
+    for (int i = 0; i < nu; i++)
+      for (int j = 0; j < nu; j++) {
+        float h = out->qH[(size_t)i * nu + j];
+        if (i == j) h += prm->alpha;
+        out->qH[(size_t)i * nu + j] = 2.f * h;
+      }
+  }
+  /* qg = 2 B^T S (A_qp x0 + Q_qp f - X_d) (SolverMPC.cpp:808-814); f = f_est only when the
+   * disturbance history exceeds 500 samples (flag bit 0), else f = 0. */
+  if (out && out->qg) {
+    float f[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t flags;
+    memcpy(&flags, rec + CMPC_REC_FLAGS, 4);
+    if (flags & 1u) f[3] = rec[CMPC_REC_FEST3];
+    sgemv(nx, 13, Aqp, x0, vec);
+    sgemv(nx, 6, Qqp, f, tmp);
+    for (int k = 0; k < N; k++)
+      for (int i = 0; i < 13; i++) {
+        const float xd = (i < 12) ? traj[12 * k + i] : 0.f;
+        vec[13 * k + i] = (vec[13 * k + i] + tmp[13 * k + i]) - xd;
+      }
+    sgemm_tn(nu, nx, nx, 2.f, Bqp, S, T); /* (2 B^T) S, a second product as in the reference */
+    sgemv(nu, nx, T, vec, out->qg);
+  }
+  if (out) {
+    memcpy(out->x0, x0, sizeof(x0));
+    memcpy(out->Adt, Adt, sizeof(Adt));
+    memcpy(out->Bdt, Bdt, sizeof(Bdt));
+    memcpy(out->Qdt, Qdt, sizeof(Qdt));
+  }
+  return CMPC_OK;
+}
+
+/* near_zero / near_one take fpt (SolverMPC.cpp:72-80) */
+static int near_zero(float a) { return (a < 0.01f && a > -.01f); }
+static int near_one(float a) { return near_zero(a - 1); }
+
+/* ---------------------------------------------------------------------------------------- */
+/* QP data + swing elimination (SolverMPC.cpp:841-950)                                       */
+/* ---------------------------------------------------------------------------------------- */
+size_t oracle_reduce_ws_bytes(int N) {
+  const size_t nv = 12u * N, nc = 20u * N;
+  return sizeof(double) * (nc * nv + 2 * nc) + sizeof(int) * (nv + nc);
+}
+
+int oracle_reduce(const float* rec, const cmpc_params* prm, const float* qH, const float* qg,
+                  oracle_red* red) {
+  void* ws = malloc(oracle_reduce_ws_bytes(prm->horizon));
+  const int st = oracle_reduce_ws(rec, prm, qH, qg, red, ws);
+  free(ws);
+  return st;
+}
+
+int oracle_reduce_ws(const float* rec, const cmpc_params* prm, const float* qH, const float* qg,
+                     oracle_red* red, void* ws) {
+  const int N = prm->horizon;
+  const int nv = 12 * N, nc = 20 * N;
+  /* fmat (:657-665) and U_b (:643-655), lb = 0 (:846-849), all as double */
+  double* A = (double*)ws;
+  double* ub = A + (size_t)nc * nv;
+  double* lb = ub + nc;
+  memset(A, 0, sizeof(double) * (size_t)nc * nv);
+  const float mu = 1.f / prm->mu;
+  const float fb[15] = {mu, 0, 1.f, -mu, 0, 1.f, 0, mu, 1.f, 0, -mu, 1.f, 0, 0, 1.f};
+  for (int i = 0; i < 4 * N; i++)
+    for (int a = 0; a < 5; a++)
+      for (int b = 0; b < 3; b++) A[(size_t)(5 * i + a) * nv + 3 * i + b] = fb[a * 3 + b];
+  for (int k = 0; k < 4 * N; k++) {
+    ub[5 * k + 0] = BIG_NUMBER;
+    ub[5 * k + 1] = BIG_NUMBER;
+    ub[5 * k + 2] = BIG_NUMBER;
+    ub[5 * k + 3] = BIG_NUMBER;
+    ub[5 * k + 4] = (float)rec_gait(rec, N, k) * prm->f_max; /* u8 * fpt */
+  }
+  for (int i = 0; i < nc; i++) lb[i] = 0.0f;
+
+  char* var_elim = red->var_elim;
+  char* con_elim = red->con_elim;
+  memset(var_elim, 0, nv);
+  memset(con_elim, 0, nc);
+  int new_vars = nv, new_cons = nc;
+  for (int i = 0; i < nc; i++) {
+    if (!(near_zero((float)lb[i]) && near_zero((float)ub[i]))) continue;
+    const double* c_row = &A[(size_t)i * nv];
+    for (int j = 0; j < nv; j++) {
+      if (near_one((float)c_row[j])) {
+        new_vars -= 3;
+        new_cons -= 5;
+        const int cs = (j * 5) / 3 - 3;
+        var_elim[j - 2] = 1; var_elim[j - 1] = 1; var_elim[j] = 1;
+        for (int t = 0; t < 5; t++) con_elim[cs + t] = 1;
+      }
+    }
+  }
+  int* var_ind = (int*)(lb + nc);
+  int* con_ind = var_ind + nv;
+  int vc = 0;
+  for (int i = 0; i < nv; i++) if (!var_elim[i]) var_ind[vc++] = i;
+  vc = 0;
+  for (int i = 0; i < nc; i++) if (!con_elim[i]) con_ind[vc++] = i;
+  for (int i = 0; i < new_vars; i++) {
+    const int olda = var_ind[i];
+    red->g[i] = (double)qg[olda];
+    for (int j = 0; j < new_vars; j++) red->H[i * new_vars + j] = (double)qH[(size_t)olda * nv + var_ind[j]];
+  }
+  for (int c = 0; c < new_cons; c++)
+    for (int s = 0; s < new_vars; s++) {
+      const float cval = (float)A[(size_t)nv * con_ind[c] + var_ind[s]]; /* :941 */
+      red->A[c * new_vars + s] = cval;
+    }
+  for (int i = 0; i < new_cons; i++) {
+    red->ub[i] = ub[con_ind[i]];
+    red->lb[i] = lb[con_ind[i]];
+  }
+  red->nv = new_vars;
+  red->nc = new_cons;
+  red->nv_full = nv;
+  red->nc_full = nc;
+  return CMPC_OK;
+}
+
+void oracle_scatter(const oracle_red* red, const double* q_red, double* q_soln) {
+  int vc = 0;
+  for (int i = 0; i < red->nv_full; i++) q_soln[i] = red->var_elim[i] ? 0.0 : q_red[vc++];
+}

@@ -1,0 +1,71 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — never linked into, loaded by, or called from the product path.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it, as the checker.
+ *
+ * CPU restatement of the reference's per-instance MPC condensation and swing-leg elimination
+ * (be2r_cmpc_unitree/src/controllers/convexMPC/SolverMPC.cpp:566-982, RobotState.cpp:9-50),
+ * reference-faithful: fp32 throughout, dense 13N x 13N weight matrix S, dense GEMMs in the order
+ * Eigen evaluates SolverMPC.cpp:806-814. The QP itself is solved by the reference's vendored
+ * qpOASES 3.2.0, compiled from /root/reference into oracle/_ref/ (see oracle/Makefile and
+ * oracle/qp_ref_shim.cpp).
+ *
+ * Parity pinning: the QP stage is pinned by the reference's own qpOASES built here; the
+ * condensation restatement cannot be pinned against the reference binary (SolverMPC.cpp needs
+ * Eigen3/FFTW3/ROS headers absent in this image) and is cross-checked instead against
+ * independent math (scipy.linalg.expm, forward simulation) in tests/test_oracle.py.
+ */
+#ifndef CMPC_ORACLE_H
+#define CMPC_ORACLE_H
+
+#include "../include/cmpc_solver.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Intermediates of one condensation (sizes for horizon N; caller-allocated, may be NULL). */
+typedef struct oracle_cond {
+  float x0[13];
+  float Adt[13 * 13];   /* row-major */
+  float Bdt[13 * 12];   /* row-major */
+  float Qdt[13 * 6];    /* row-major */
+  float* qH;            /* [12N * 12N] row-major, may be NULL */
+  float* qg;            /* [12N] */
+} oracle_cond;
+
+/* Reduced QP exactly as handed to qpOASES (SolverMPC.cpp:841-950). */
+typedef struct oracle_red {
+  int nv, nc;           /* reduced sizes */
+  int nv_full, nc_full;
+  double* H;            /* [nv*nv] row-major (capacity 144 N^2) */
+  double* g;            /* [nv] */
+  double* A;            /* [nc*nv] row-major (capacity 240 N^2) */
+  double* lb;           /* [nc] */
+  double* ub;           /* [nc] */
+  char* var_elim;       /* [12N] */
+  char* con_elim;       /* [20N] */
+} oracle_red;
+
+/* Condense one record (layout: include/cmpc_solver.h). qH/qg computed as the reference does. */
+int oracle_condense(const float* rec, const cmpc_params* prm, oracle_cond* out);
+
+/* Same with a caller-provided workspace of oracle_condense_ws_bytes(N) bytes (no malloc). */
+size_t oracle_condense_ws_bytes(int horizon);
+int oracle_condense_ws(const float* rec, const cmpc_params* prm, oracle_cond* out, void* ws);
+
+/* Elimination + reduction from a condensed (qH, qg) and the record's gait. */
+int oracle_reduce(const float* rec, const cmpc_params* prm, const float* qH, const float* qg,
+                  oracle_red* red);
+
+size_t oracle_reduce_ws_bytes(int horizon);
+int oracle_reduce_ws(const float* rec, const cmpc_params* prm, const float* qH, const float* qg,
+                     oracle_red* red, void* ws);
+
+/* Scatter a reduced solution back to q_soln[12N] (0 for eliminated), SolverMPC.cpp:970-982. */
+void oracle_scatter(const oracle_red* red, const double* q_red, double* q_soln);
+
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,148 @@
+"""TEST INFRASTRUCTURE ONLY — the CPU checker. Imported only by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg; never by the product package.
+
+ctypes front-end to:
+  * ``oracle/_build/libcmpc_oracle.so`` — fp32 restatement of the reference condensation and
+    swing elimination (``SolverMPC.cpp:566-982``), see ``cmpc_oracle.c``;
+  * ``oracle/_ref/libcmpc_ref.so`` — the same chained with the reference's own qpOASES 3.2.0
+    (compiled from ``/root/reference`` by ``oracle/Makefile``), i.e. the whole reference
+    ``solve_mpc`` per instance.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "_build", "libcmpc_oracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libcmpc_ref.so")
+QPOASES_SRC = "/root/reference/be2r_cmpc_unitree/src/third_party/qpOASES"
+
+_f = ctypes.POINTER(ctypes.c_float)
+_d = ctypes.POINTER(ctypes.c_double)
+_i = ctypes.POINTER(ctypes.c_int)
+
+
+class OracleCond(ctypes.Structure):
+    _fields_ = [("x0", ctypes.c_float * 13), ("Adt", ctypes.c_float * 169),
+                ("Bdt", ctypes.c_float * 156), ("Qdt", ctypes.c_float * 78),
+                ("qH", _f), ("qg", _f)]
+
+
+class OracleRed(ctypes.Structure):
+    _fields_ = [("nv", ctypes.c_int), ("nc", ctypes.c_int), ("nv_full", ctypes.c_int),
+                ("nc_full", ctypes.c_int), ("H", _d), ("g", _d), ("A", _d), ("lb", _d),
+                ("ub", _d), ("var_elim", ctypes.c_char_p), ("con_elim", ctypes.c_char_p)]
+
+
+def build(force: bool = False) -> None:
+    """make -C oracle (own restatement always; _ref only when /root/reference is present)."""
+    args = ["make", "-C", HERE, "-j8", "oracle"]
+    if os.path.isdir(QPOASES_SRC):
+        args.append("ref")
+    if force:
+        subprocess.run(["make", "-C", HERE, "clean"], check=True, capture_output=True)
+    subprocess.run(args, check=True, capture_output=True)
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        _lib = ctypes.CDLL(ORACLE_SO)
+        _lib.oracle_condense.argtypes = [_f, ctypes.c_void_p, ctypes.POINTER(OracleCond)]
+        _lib.oracle_reduce.argtypes = [_f, ctypes.c_void_p, _f, _f, ctypes.POINTER(OracleRed)]
+    return _lib
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_SO)
+
+
+def ref():
+    global _ref
+    if _ref is None:
+        if not os.path.exists(REF_SO):
+            raise FileNotFoundError(f"{REF_SO} missing: run `make -C oracle ref` where "
+                                    f"/root/reference is present")
+        _ref = ctypes.CDLL(REF_SO)
+        _ref.qpref_solve.argtypes = [ctypes.c_int, ctypes.c_int, _d, _d, _d, _d, _d,
+                                     ctypes.c_int, _d, _i, _i]
+        _ref.ref_solve_batch.argtypes = [_f, ctypes.c_int, ctypes.c_void_p, _d, _i, _i, ctypes.c_int]
+        _ref.oracle_condense.argtypes = [_f, ctypes.c_void_p, ctypes.POINTER(OracleCond)]
+    return _ref
+
+
+def _fp(a):
+    return a.ctypes.data_as(_f)
+
+
+def condense(rec: np.ndarray, prm, full: bool = True):
+    """Reference-faithful fp32 condensation of one record -> dict(x0, Adt, Bdt, Qdt, qH, qg)."""
+    N = prm.horizon
+    rec = np.ascontiguousarray(rec, np.float32)
+    qH = np.zeros((12 * N, 12 * N), np.float32)
+    qg = np.zeros(12 * N, np.float32)
+    c = OracleCond()
+    c.qH = _fp(qH) if full else None
+    c.qg = _fp(qg)
+    st = lib().oracle_condense(_fp(rec), ctypes.byref(prm), ctypes.byref(c))
+    if st != 0:
+        raise ValueError(f"oracle_condense status {st}")
+    return dict(x0=np.array(c.x0, np.float32), Adt=np.array(c.Adt, np.float32).reshape(13, 13),
+                Bdt=np.array(c.Bdt, np.float32).reshape(13, 12),
+                Qdt=np.array(c.Qdt, np.float32).reshape(13, 6), qH=qH, qg=qg)
+
+
+def reduce(rec: np.ndarray, prm, qH: np.ndarray, qg: np.ndarray):
+    """Swing elimination (SolverMPC.cpp:859-950) -> dict(H, g, A, lb, ub, var_elim)."""
+    N = prm.horizon
+    nv, nc = 12 * N, 20 * N
+    H = np.zeros(nv * nv); g = np.zeros(nv); A = np.zeros(nc * nv)
+    lb = np.zeros(nc); ub = np.zeros(nc)
+    ve = ctypes.create_string_buffer(nv); ce = ctypes.create_string_buffer(nc)
+    r = OracleRed()
+    r.H, r.g, r.A = H.ctypes.data_as(_d), g.ctypes.data_as(_d), A.ctypes.data_as(_d)
+    r.lb, r.ub = lb.ctypes.data_as(_d), ub.ctypes.data_as(_d)
+    r.var_elim = ctypes.cast(ve, ctypes.c_char_p)
+    r.con_elim = ctypes.cast(ce, ctypes.c_char_p)
+    lib().oracle_reduce(_fp(np.ascontiguousarray(rec, np.float32)), ctypes.byref(prm),
+                        _fp(np.ascontiguousarray(qH, np.float32)),
+                        _fp(np.ascontiguousarray(qg, np.float32)), ctypes.byref(r))
+    n, m = r.nv, r.nc
+    return dict(H=H[:n * n].reshape(n, n), g=g[:n].copy(), A=A[:m * n].reshape(m, n),
+                lb=lb[:m].copy(), ub=ub[:m].copy(),
+                var_elim=np.frombuffer(ve.raw, np.uint8)[:nv].astype(bool))
+
+
+def qpoases(H, g, A, lb, ub, nwsr_max: int = 100):
+    """The reference's QP call (SolverMPC.cpp:955-964) -> (x, nWSR, rval_init, rval_primal)."""
+    n, m = H.shape[0], A.shape[0]
+    x = np.zeros(max(n, 1))
+    nw = ctypes.c_int(0)
+    ri = ctypes.c_int(0)
+    args = [np.ascontiguousarray(a, np.float64) for a in (H, g, A, lb, ub)]
+    r2 = ref().qpref_solve(n, m, *[a.ctypes.data_as(_d) for a in args], nwsr_max,
+                           x.ctypes.data_as(_d), ctypes.byref(nw), ctypes.byref(ri))
+    return x[:n], nw.value, ri.value, r2
+
+
+def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1):
+    """Reference pipeline over a batch -> (q_soln [B, 12N] f64, status [B], nWSR [B])."""
+    B = records.shape[0]
+    N = prm.horizon
+    records = np.ascontiguousarray(records, np.float32)
+    q = np.zeros((B, 12 * N))
+    st = np.zeros(B, np.int32)
+    nw = np.zeros(B, np.int32)
+    ref().ref_solve_batch(_fp(records), B, ctypes.byref(prm), q.ctypes.data_as(_d),
+                          st.ctypes.data_as(_i), nw.ctypes.data_as(_i), int(nthreads))
+    return q, st, nw

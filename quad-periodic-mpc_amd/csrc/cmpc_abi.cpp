@@ -1,0 +1,439 @@
+// cmpc_abi.cpp — the C ABI of libcmpc_hip.so (declared in include/cmpc_solver.h).
+//
+//  * cmpc_batch_*: reentrant batched API, one handle per HIP stream, device scratch allocated
+//    at create time (never inside solve, so a caller may capture solve into a hipGraph).
+//  * setup_problem / update_problem_data(_floats) / update_solver_settings / update_x_drag /
+//    get_solution: the reference's single-instance interface (convexMPC_interface.h:44-52) with
+//    the same call protocol and semantics, implemented over a batch-1 handle.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cmpc_solver.h"
+#include "cmpc_kernels.h"
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(const char* what, hipError_t e) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return -(int)e - 1000;
+}
+}  // namespace
+
+struct cmpc_batch {
+  cmpc_params prm;
+  cmpc::KParams kp;
+  int max_batch = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int* d_work = nullptr;
+  // staging for the host-pointer entry point (allocated lazily, sized max_batch)
+  float* d_rec = nullptr;
+  float* d_forces = nullptr;
+  uint8_t* d_status = nullptr;
+  int32_t* d_iters = nullptr;
+  // optional per-launch timing (cmpc_batch_enable_timing)
+  std::vector<hipEvent_t> ev;
+  int ev_steps = 0, ev_next = 0;
+};
+
+static cmpc::KParams make_kparams(const cmpc_params& p) {
+  cmpc::KParams k{};
+  k.dt = p.dt;
+  k.mu_inv = 1.f / p.mu;  // fpt mu = 1.f / setup->mu (SolverMPC.cpp:657)
+  k.f_max = p.f_max;
+  k.alpha2 = 2.f * p.alpha;
+  for (int i = 0; i < 12; i++) k.wts[i] = p.weights[i];
+  k.N = p.horizon;
+  k.rec_words = CMPC_REC_WORDS(p.horizon);
+  k.max_iter = p.max_iter > 0 ? p.max_iter : 100;
+  return k;
+}
+
+extern "C" int cmpc_record_words(int horizon) { return CMPC_REC_WORDS(horizon); }
+
+extern "C" const char* cmpc_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int cmpc_batch_set_params(cmpc_batch* h, const cmpc_params* prm) {
+  if (!h || !prm) return -1;
+  if (prm->horizon < 1 || prm->horizon > CMPC_MAX_HORIZON) {
+    g_last_error = "horizon out of range";
+    return -2;
+  }
+  if (12 * prm->horizon > 128) {
+    g_last_error = "horizon > 10 with all legs in stance needs the 4-wave class (not built)";
+    // still accepted: instances with n > 128 reduced variables report CMPC_BAD_INPUT
+  }
+  h->prm = *prm;
+  h->kp = make_kparams(*prm);
+  return 0;
+}
+
+extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int max_batch,
+                                 void* hip_stream) {
+  if (!out || !prm || max_batch < 1) return -1;
+  auto* h = new cmpc_batch();
+  if (int r = cmpc_batch_set_params(h, prm); r != 0) {
+    delete h;
+    return r;
+  }
+  h->max_batch = max_batch;
+  hipError_t e;
+  if (hip_stream) {
+    h->stream = (hipStream_t)hip_stream;
+  } else {
+    e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete h; return fail("hipStreamCreate", e); }
+    h->own_stream = true;
+  }
+  e = hipMalloc(&h->d_work, sizeof(int) * cmpc::work_ints(max_batch));
+  if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("hipMalloc(work)", e); }
+  *out = h;
+  return 0;
+}
+
+extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
+  if (!h) return;
+  if (h->d_work) (void)hipFree(h->d_work);
+  if (h->d_rec) (void)hipFree(h->d_rec);
+  if (h->d_forces) (void)hipFree(h->d_forces);
+  if (h->d_status) (void)hipFree(h->d_status);
+  if (h->d_iters) (void)hipFree(h->d_iters);
+  for (auto e : h->ev) (void)hipEventDestroy(e);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+extern "C" void* cmpc_batch_stream(cmpc_batch* h) { return h ? (void*)h->stream : nullptr; }
+
+extern "C" int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int batch, float* d_forces,
+                                uint8_t* d_status, int32_t* d_iters) {
+  if (!h || batch < 0 || batch > h->max_batch || (!d_records && batch) || (!d_forces && batch) ||
+      (!d_status && batch)) {
+    g_last_error = "cmpc_batch_solve: bad arguments";
+    return -1;
+  }
+  hipEvent_t* ev = nullptr;
+  if (h->ev_steps > 0 && h->ev_next < h->ev_steps) ev = &h->ev[3 * h->ev_next++];
+  hipError_t e = cmpc::launch_solve(d_records, batch, h->kp, d_forces, d_status, d_iters, h->d_work,
+                                    h->max_batch, h->stream, ev);
+  if (e != hipSuccess) return fail("launch_solve", e);
+  return 0;
+}
+
+extern "C" int cmpc_batch_enable_timing(cmpc_batch* h, int steps) {
+  if (!h || steps < 0) return -1;
+  for (auto e : h->ev) (void)hipEventDestroy(e);
+  h->ev.assign(3 * (size_t)steps, nullptr);
+  for (auto& e : h->ev)
+    if (hipError_t r = hipEventCreate(&e); r != hipSuccess) return fail("hipEventCreate", r);
+  h->ev_steps = steps;
+  h->ev_next = 0;
+  return 0;
+}
+
+extern "C" int cmpc_batch_read_timing(cmpc_batch* h, float* ms, int* steps_recorded,
+                                      int* class1_overflow) {
+  if (!h) return -1;
+  hipError_t e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) return fail("sync", e);
+  for (int i = 0; i < h->ev_next; i++) {
+    float a = 0.f, b = 0.f;
+    (void)hipEventElapsedTime(&a, h->ev[3 * i], h->ev[3 * i + 1]);
+    (void)hipEventElapsedTime(&b, h->ev[3 * i + 1], h->ev[3 * i + 2]);
+    ms[2 * i] = a;
+    ms[2 * i + 1] = b;
+  }
+  if (steps_recorded) *steps_recorded = h->ev_next;
+  if (class1_overflow) {
+    int c = 0;
+    e = hipMemcpy(&c, h->d_work, sizeof(int), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail("D2H", e);
+    *class1_overflow = c;
+  }
+  h->ev_next = 0;
+  return 0;
+}
+
+extern "C" int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int batch, float* d_H,
+                                   float* d_g) {
+  if (!h || batch < 0 || batch > h->max_batch) return -1;
+  hipError_t e = cmpc::launch_condense(d_records, batch, h->kp, d_H, d_g, h->stream);
+  if (e != hipSuccess) return fail("launch_condense", e);
+  return 0;
+}
+
+static int ensure_staging(cmpc_batch* h) {
+  if (h->d_rec) return 0;
+  const size_t words = (size_t)CMPC_REC_WORDS(CMPC_MAX_HORIZON) * h->max_batch;
+  hipError_t e;
+  if ((e = hipMalloc(&h->d_rec, words * sizeof(float))) != hipSuccess) return fail("hipMalloc", e);
+  if ((e = hipMalloc(&h->d_forces, (size_t)12 * CMPC_MAX_HORIZON * h->max_batch * sizeof(float))) != hipSuccess)
+    return fail("hipMalloc", e);
+  if ((e = hipMalloc(&h->d_status, (size_t)h->max_batch)) != hipSuccess) return fail("hipMalloc", e);
+  if ((e = hipMalloc(&h->d_iters, sizeof(int32_t) * h->max_batch)) != hipSuccess) return fail("hipMalloc", e);
+  return 0;
+}
+
+extern "C" int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int batch, float* forces,
+                                     uint8_t* status, int32_t* iters) {
+  if (!h || batch < 0 || batch > h->max_batch) return -1;
+  if (batch == 0) return 0;
+  if (int r = ensure_staging(h)) return r;
+  const int N = h->prm.horizon;
+  const size_t rw = (size_t)CMPC_REC_WORDS(N);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(h->d_rec, records, rw * batch * sizeof(float), hipMemcpyHostToDevice, h->stream)) != hipSuccess)
+    return fail("H2D", e);
+  if (int r = cmpc_batch_solve(h, h->d_rec, batch, h->d_forces, h->d_status, h->d_iters)) return r;
+  if ((e = hipMemcpyAsync(forces, h->d_forces, sizeof(float) * 12 * N * batch, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+    return fail("D2H", e);
+  if (status && (e = hipMemcpyAsync(status, h->d_status, batch, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+    return fail("D2H", e);
+  if (iters && (e = hipMemcpyAsync(iters, h->d_iters, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+    return fail("D2H", e);
+  if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail("sync", e);
+  return 0;
+}
+
+// =============================================================================================
+// Reference single-instance interface (convexMPC_interface.cpp + the solve_mpc globals).
+// =============================================================================================
+extern "C" {
+// Defined by the reference's caller (ConvexMPCLocomotion.cpp:610; be2r_cmpc_unitree_node.cpp:6);
+// weak here so the library also loads on its own. The host program's definitions win.
+__attribute__((weak)) float f_ext[6] = {0, 0, 0, 0, 0, 0};
+__attribute__((weak)) float simulation_time = 0.f;
+}
+
+namespace {
+struct SingleState {
+  std::mutex mu;
+  cmpc_params cfg{};              // problem_configuration (convexMPC_interface.cpp:10)
+  bool configured = false;
+  // update_data_t fields (convexMPC_interface.h:23-41)
+  float p[3]{}, v[3]{}, q[4]{}, w[3]{}, r[12]{};
+  float roll = 0, pitch = 0, yaw = 0, alpha = 0, x_drag = 0;
+  float weights[12]{};
+  std::vector<float> traj;
+  std::vector<unsigned char> gait;
+  int max_iterations = 0, use_jcqp = 0;
+  double rho = 0, sigma = 0, solver_alpha = 0, terminate = 0;
+  // solve_mpc state
+  std::vector<double> q_soln;
+  int has_solved = 0;
+  cmpc_batch* h = nullptr;
+  int h_horizon = -1;
+  // periodic-disturbance estimator state (SolverMPC.cpp:390-398, 555-563, 688-798)
+  std::vector<float> time_history, diff_history;
+  double est_stat = 0, est_amp = 0, est_freq = 0, est_phase = 0;
+  float f_est[6]{}, f_est_smoothed[6]{}, f_est_static[6]{};
+};
+SingleState g;
+
+// gaussian_filter (SolverMPC.cpp:404-437): float kernel, radius ceil(3 sigma), edge clamp
+std::vector<double> gaussian_filter(const std::vector<double>& data, float sigma) {
+  const int radius = (int)std::ceil(3 * sigma);
+  std::vector<float> kernel(2 * radius + 1);
+  float sum = 0.0;
+  for (int i = -radius; i <= radius; i++) {
+    const float value = std::exp(-0.5 * (i * i) / (sigma * sigma));
+    kernel[i + radius] = value;
+    sum += value;
+  }
+  for (auto& k : kernel) k /= sum;
+  const int n = (int)data.size();
+  std::vector<double> out(n, 0.0);
+  for (int i = 0; i < n; i++) {
+    double acc = 0.0;
+    for (int j = -radius; j <= radius; j++) {
+      int idx = i + j;
+      idx = idx < 0 ? 0 : (idx >= n ? n - 1 : idx);
+      acc += data[idx] * kernel[j + radius];
+    }
+    out[i] = acc;
+  }
+  return out;
+}
+
+// fit_sin initial guesses (SolverMPC.cpp:478-541): peak |rfft| bin >= 1, amp = sqrt2 std,
+// offset = mean, phase = 0. The r2c magnitudes are evaluated by a direct DFT (W = 400 bins).
+void fit_sin(const std::vector<double>& tt, const std::vector<double>& yy, double& amp,
+             double& freq, double& phase, double& offset) {
+  const int n = (int)tt.size();
+  const double dt = tt[1] - tt[0];
+  int best = 1;
+  double best_mag = -1.0;
+  for (int k = 1; k <= n / 2; k++) {
+    std::complex<double> acc(0, 0);
+    for (int t = 0; t < n; t++) {
+      const double ang = -2.0 * M_PI * (double)k * (double)t / (double)n;
+      acc += yy[t] * std::complex<double>(std::cos(ang), std::sin(ang));
+    }
+    const double mag = std::abs(acc);
+    if (k == 1 || mag > best_mag) { best_mag = mag; best = k; }
+  }
+  const double f = (best <= n / 2) ? best / (n * dt) : (best - n) / (n * dt);
+  double m = 0;
+  for (double y : yy) m += y;
+  m /= n;
+  double s = 0;
+  for (double y : yy) s += (y - m) * (y - m);
+  s = std::sqrt(s / n);
+  amp = s * std::sqrt(2.0);
+  offset = m;
+  phase = 0.0;
+  freq = (2 * M_PI * std::fabs(f)) / (2 * M_PI);
+}
+
+void estimator_step(SingleState& s) {
+  // SolverMPC.cpp:692-798
+  s.diff_history.push_back(f_ext[3]);
+  s.time_history.push_back(simulation_time);
+  const size_t window = 400;
+  if (s.time_history.size() >= window) {
+    if (s.time_history.size() <= 500) {
+      std::vector<double> tw(s.time_history.end() - window, s.time_history.end());
+      std::vector<double> dw(s.diff_history.end() - window, s.diff_history.end());
+      auto blurred = gaussian_filter(dw, 7.0f);
+      auto very_blurred = gaussian_filter(dw, 27.0f);
+      std::vector<double> band(dw.size());
+      for (size_t i = 0; i < dw.size(); i++) band[i] = blurred[i] - very_blurred[i];
+      fit_sin(tw, band, s.est_amp, s.est_freq, s.est_phase, s.est_stat);
+    }
+    // NB: '+' as in the reference (SolverMPC.cpp:766)
+    const float comp = (float)(s.est_amp + std::sin(2 * M_PI * simulation_time * s.est_freq + s.est_phase));
+    s.f_est[3] = comp;
+  }
+  for (int i = 0; i < 6; i++) s.f_est_smoothed[i] = 0.95f * s.f_est_smoothed[i] + 0.05f * s.f_est[i];
+  s.f_est_static[3] = 0.97f * s.f_est_static[3] + 0.03f * f_ext[3];
+}
+
+void solve_single(SingleState& s) {
+  const int N = s.cfg.horizon;
+  if (N < 1 || N > CMPC_MAX_HORIZON) {
+    std::fprintf(stderr, "[cmpc] horizon %d out of range\n", N);
+    return;
+  }
+  if (!s.h || s.h_horizon != N) {
+    if (s.h) cmpc_batch_destroy(s.h);
+    s.h = nullptr;
+    if (cmpc_batch_create(&s.h, &s.cfg, 1, nullptr) != 0) {
+      std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
+      return;
+    }
+    s.h_horizon = N;
+  }
+  cmpc_params prm = s.cfg;
+  for (int i = 0; i < 12; i++) prm.weights[i] = s.weights[i];
+  prm.alpha = s.alpha;
+  prm.max_iter = 100;  // nWSR = 100 (SolverMPC.cpp:854)
+  cmpc_batch_set_params(s.h, &prm);
+
+  estimator_step(s);
+
+  std::vector<float> rec(CMPC_REC_WORDS(N), 0.f);
+  std::memcpy(&rec[CMPC_REC_P], s.p, sizeof(s.p));
+  std::memcpy(&rec[CMPC_REC_V], s.v, sizeof(s.v));
+  std::memcpy(&rec[CMPC_REC_Q], s.q, sizeof(s.q));
+  std::memcpy(&rec[CMPC_REC_W], s.w, sizeof(s.w));
+  std::memcpy(&rec[CMPC_REC_R], s.r, sizeof(s.r));
+  rec[CMPC_REC_RPY + 0] = s.roll;
+  rec[CMPC_REC_RPY + 1] = s.pitch;
+  rec[CMPC_REC_RPY + 2] = s.yaw;
+  rec[CMPC_REC_XDRAG] = s.x_drag;
+  rec[CMPC_REC_FEST3] = s.f_est[3];
+  const uint32_t flags = (s.time_history.size() > 500) ? 1u : 0u;  // SolverMPC.cpp:808
+  std::memcpy(&rec[CMPC_REC_FLAGS], &flags, 4);
+  std::memcpy(&rec[CMPC_REC_TRAJ(N)], s.traj.data(), sizeof(float) * 12 * N);
+  std::memcpy(&rec[CMPC_REC_GAIT(N)], s.gait.data(), 4 * N);
+
+  std::vector<float> forces(12 * N);
+  uint8_t st = 0;
+  if (cmpc_batch_solve_host(s.h, rec.data(), 1, forces.data(), &st, nullptr) != 0) {
+    std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
+    return;
+  }
+  if (st != CMPC_OK) std::printf("failed to solve!\n");  // SolverMPC.cpp:967
+  s.q_soln.assign(12 * N, 0.0);
+  for (int i = 0; i < 12 * N; i++) s.q_soln[i] = forces[i];
+  s.has_solved = 1;
+}
+}  // namespace
+
+extern "C" void setup_problem(double dt, int horizon, double mu, double f_max) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  g.cfg.dt = (float)dt;
+  g.cfg.horizon = horizon;
+  g.cfg.mu = (float)mu;
+  g.cfg.f_max = (float)f_max;
+  g.configured = true;
+  // resize_qp_mats (SolverMPC.cpp:149-250): the reference re-allocates q_soln here
+  g.traj.assign(12 * (horizon > 0 ? horizon : 1) + 12 * CMPC_MAX_HORIZON, 0.f);
+  g.gait.assign(4 * CMPC_MAX_HORIZON + 4, 0);
+  if (horizon > 19) std::fprintf(stderr, "[cmpc] horizon %d > 19: reference c2qp would throw; cap lifted\n", horizon);
+}
+
+extern "C" void update_solver_settings(int max_iter, double rho, double sigma, double solver_alpha,
+                                       double terminate, double use_jcqp) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  g.max_iterations = max_iter;
+  g.rho = rho;
+  g.sigma = sigma;
+  g.solver_alpha = solver_alpha;
+  g.terminate = terminate;
+  g.use_jcqp = use_jcqp > 1.5 ? 2 : (use_jcqp > 0.5 ? 1 : 0);
+  if (g.use_jcqp != 0) std::fprintf(stderr, "[cmpc] use_jcqp=%d: JCQP is not built; dense active-set QP used\n", g.use_jcqp);
+}
+
+extern "C" void update_problem_data_floats(float* p, float* v, float* q, float* w, float* r, float roll,
+                                           float pitch, float yaw, float* weights, float* state_trajectory,
+                                           float alpha, int* gait) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  const int N = g.cfg.horizon;
+  g.alpha = alpha;
+  g.roll = roll;
+  g.pitch = pitch;
+  g.yaw = yaw;
+  for (int i = 0; i < 4 * N; i++) g.gait[i] = (unsigned char)gait[i];  // mint_to_u8
+  std::memcpy(g.p, p, sizeof(float) * 3);
+  std::memcpy(g.v, v, sizeof(float) * 3);
+  std::memcpy(g.q, q, sizeof(float) * 4);
+  std::memcpy(g.w, w, sizeof(float) * 3);
+  std::memcpy(g.r, r, sizeof(float) * 12);
+  std::memcpy(g.weights, weights, sizeof(float) * 12);
+  std::memcpy(g.traj.data(), state_trajectory, sizeof(float) * 12 * N);
+  solve_single(g);
+}
+
+extern "C" void update_problem_data(double* p, double* v, double* q, double* w, double* r, double yaw,
+                                    double* weights, double* state_trajectory, double alpha, int* gait) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  const int N = g.cfg.horizon;
+  for (int i = 0; i < 3; i++) { g.p[i] = (float)p[i]; g.v[i] = (float)v[i]; g.w[i] = (float)w[i]; }
+  for (int i = 0; i < 4; i++) g.q[i] = (float)q[i];
+  for (int i = 0; i < 12; i++) { g.r[i] = (float)r[i]; g.weights[i] = (float)weights[i]; }
+  g.yaw = (float)yaw;
+  for (int i = 0; i < 12 * N; i++) g.traj[i] = (float)state_trajectory[i];
+  g.alpha = (float)alpha;
+  for (int i = 0; i < 4 * N; i++) g.gait[i] = (unsigned char)gait[i];
+  solve_single(g);
+}
+
+void update_x_drag(float x_drag) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  g.x_drag = x_drag;
+}
+
+extern "C" double get_solution(int index) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (!g.has_solved) return 0.f;
+  return g.q_soln[index];
+}

@@ -1,0 +1,880 @@
+// cmpc_kernels.hip — fused condensation + friction-cone QP, one MPC instance per workgroup.
+//
+// What one workgroup computes is one call of the reference's solve_mpc()
+// (be2r_cmpc_unitree/src/controllers/convexMPC/SolverMPC.cpp:566-982):
+//   RobotState::set + quat_to_rpy (RobotState.cpp:9-50, SolverMPC.cpp:352-361)
+//   ct_ss_mats + c2qp discretisation (SolverMPC.cpp:260-279, 96-107)
+//   condensation qH = 2(B_qp' S B_qp + alpha I), qg = 2 B_qp' S (A_qp x0 + Q_qp f - X_d)
+//     (SolverMPC.cpp:118-139, 806-814), built directly in reduced form: only stance-leg
+//     force variables (the reference's elimination, SolverMPC.cpp:859-950)
+//   the dense friction-pyramid QP (qpOASES QProblem::init in the reference,
+//     SolverMPC.cpp:955-969) solved exactly by a Goldfarb-Idnani dual active-set method
+//   scatter back to q_soln[12N] with zeros for swing legs (SolverMPC.cpp:970-982).
+//
+// MI355X mapping:
+//   * workgroup = W wavefronts = 64W threads; thread v owns reduced variable v, i.e. ROW v of
+//     H, of its Cholesky factor U, and of J = U^{-1}, held in VGPRs (NV + 1 fp32 slots).
+//   * condensation: thread v runs the 13-state backward recursion for its own force column,
+//     z_i = S A^{i-k_v} b_v + A' z_{i+1}, with A^k b in closed form (A - I is nilpotent,
+//     (A-I)^3 = 0), and fills H[v][w] = 2 b_w' z_{blk(w)} for every w in blocks >= k_v.
+//   * Cholesky / inverse are right-looking, one pivot row broadcast through LDS per step;
+//     the raw factor rows live in LDS (region M) and are reused as the QP's R matrix.
+//   * QP: constraints are the 6 one-sided rows of each stance foot's pyramid; J (= L^-T Q) in
+//     registers is updated by Givens rotations (column ops = independent per thread/row).
+// Everything is fp32 (the reference condenses in fp32: common_types.h:14).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cmpc_kernels.h"
+
+namespace cmpc {
+
+namespace {
+
+constexpr int MAXN = CMPC_MAX_HORIZON;
+constexpr float kBigF = 3.0e38f;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+// argmin with deterministic tie-break on the smaller index
+__device__ __forceinline__ void wave_argmin(float& v, int& i) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float ov = __shfl_xor(v, off, 64);
+    const int oi = __shfl_xor(i, off, 64);
+    if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+}
+// inclusive suffix sum over lanes: s_l = sum_{m >= l} v_m
+__device__ __forceinline__ float wave_suffix_sum(float v, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float t = __shfl_down(v, off, 64);
+    if (lane + off < 64) v += t;
+  }
+  return v;
+}
+
+template <int W>
+__device__ __forceinline__ void bsync() {
+  __syncthreads();
+}
+
+template <int W>
+struct Shared {
+  static constexpr int NV = 64 * W;
+  static constexpr int LDM = NV + 4;      // row stride of M (16-B aligned rows)
+  float M[NV * LDM];                      // raw Cholesky rows, then R (row-major, q x q)
+  float BdtT[12][16];                     // Bdt columns (13 used)
+  float traj[MAXN * 12];
+  float E[MAXN][16];                      // state error e_i = x_{i+1}(U=0) - X_d,i
+  float ZE[MAXN][16];                     // gradient recursion ze_i
+  float bufA[2][NV + 4];                  // pivot-row / J-row broadcast buffers
+  float bufB[NV + 4];
+  float dfull[NV + 4];                    // d = J' n+
+  float dmask[NV + 4];                    // d with entries < q zeroed
+  float tsv[NV + 4];                      // suffix norms
+  float cs[2 * NV + 8];                   // Givens (c, s) pairs
+  float xs[NV + 4];                       // current primal iterate
+  float rvec[NV + 4];                     // dual step r
+  float u[NV + 4];                        // duals of the active set
+  int act[NV + 4];                        // active constraint ids (6 * foot + type)
+  float red_f[8];
+  int red_i[8];
+  float sub[4 * MAXN];                    // ub of each stance foot step (gait * f_max)
+  int sfs[4 * MAXN];                      // stance foot step ids, in order
+  int blkbase[MAXN + 2];                  // first reduced variable of each horizon step
+  unsigned char varblk[NV];
+  unsigned char varcol[NV];
+  unsigned char stance[4 * MAXN];
+  unsigned char cflag[6 * 4 * MAXN];      // active flags per constraint id
+  int ctrl[4];
+};
+
+template <int W>
+__device__ __forceinline__ float block_sum(float v, Shared<W>& sh) {
+  v = wave_sum(v);
+  if constexpr (W == 1) {
+    return v;
+  } else {
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh.red_f[wv] = v;
+    bsync<W>();
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < W; i++) s += sh.red_f[i];
+    bsync<W>();
+    return s;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ float block_max(float v, Shared<W>& sh) {
+  v = wave_max(v);
+  if constexpr (W == 1) {
+    return v;
+  } else {
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh.red_f[wv] = v;
+    bsync<W>();
+    float s = sh.red_f[0];
+#pragma unroll
+    for (int i = 1; i < W; i++) s = fmaxf(s, sh.red_f[i]);
+    bsync<W>();
+    return s;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void block_argmin(float& v, int& idx, Shared<W>& sh) {
+  wave_argmin(v, idx);
+  if constexpr (W > 1) {
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh.red_f[wv] = v; sh.red_i[wv] = idx; }
+    bsync<W>();
+    v = sh.red_f[0];
+    idx = sh.red_i[0];
+#pragma unroll
+    for (int i = 1; i < W; i++) {
+      const float ov = sh.red_f[i];
+      const int oi = sh.red_i[i];
+      if (ov < v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    }
+    bsync<W>();
+  }
+}
+
+template <int W>
+__device__ __forceinline__ float block_suffix_sum(float v, Shared<W>& sh) {
+  const int lane = threadIdx.x & 63;
+  v = wave_suffix_sum(v, lane);
+  if constexpr (W > 1) {
+    const int wv = threadIdx.x >> 6;
+    if (lane == 0) sh.red_f[wv] = v;  // wave total
+    bsync<W>();
+    float add = 0.f;
+#pragma unroll
+    for (int i = 0; i < W; i++) add += (i > wv) ? sh.red_f[i] : 0.f;
+    bsync<W>();
+    v += add;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Discretised model pieces (SolverMPC.cpp:260-279 + 96-107 in closed form; A_c^3 = 0 so
+// expm(dt [A B Q; 0]) = I + M + M^2/2 + M^3/6 exactly):
+//   Adt = I + N1,  N1 = dt A_c + dt^2/2 A_c^2   (16 structural nonzeros, see n1_* below)
+//   Bdt = dt B_c + dt^2/2 A_c B_c + dt^3/6 A_c^2 B_c
+// ---------------------------------------------------------------------------------------------
+struct Model {
+  float R[9];      // body rotation (Eigen toRotationMatrix of q, w-first), R_yaw = R
+  float n1r[9];    // N1[0..2][6..8] = dt * R^T
+  float dt, dth, xdrag;  // dt, dt^2/2, x_drag
+};
+
+// y = N1 x   (13-vectors)
+__device__ __forceinline__ void n1_mul(const Model& m, const float* x, float* y) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) y[i] = m.n1r[i * 3 + 0] * x[6] + m.n1r[i * 3 + 1] * x[7] + m.n1r[i * 3 + 2] * x[8];
+  y[3] = m.dt * x[9];
+  y[4] = m.dt * x[10];
+  y[5] = m.dt * x[11] + (m.dth * m.xdrag) * x[9] + m.dth * x[12];
+#pragma unroll
+  for (int i = 6; i < 11; i++) y[i] = 0.f;
+  y[11] = (m.dt * m.xdrag) * x[9] + m.dt * x[12];
+  y[12] = 0.f;
+}
+
+// z <- w .* e + Adt' z   (in place on z)
+__device__ __forceinline__ void recur(const Model& m, const float* wts, const float* e, float* z) {
+  float t[13];
+#pragma unroll
+  for (int j = 0; j < 13; j++) t[j] = z[j];
+  // N1' z
+  const float c6 = m.n1r[0] * t[0] + m.n1r[3] * t[1] + m.n1r[6] * t[2];
+  const float c7 = m.n1r[1] * t[0] + m.n1r[4] * t[1] + m.n1r[7] * t[2];
+  const float c8 = m.n1r[2] * t[0] + m.n1r[5] * t[1] + m.n1r[8] * t[2];
+  const float c9 = m.dt * t[3] + (m.dt * m.xdrag) * t[11] + (m.dth * m.xdrag) * t[5];
+  const float c10 = m.dt * t[4];
+  const float c11 = m.dt * t[5];
+  const float c12 = m.dt * t[11] + m.dth * t[5];
+#pragma unroll
+  for (int j = 0; j < 13; j++) z[j] = wts[j] * e[j] + t[j];
+  z[6] += c6; z[7] += c7; z[8] += c8; z[9] += c9; z[10] += c10; z[11] += c11; z[12] += c12;
+}
+
+__device__ __forceinline__ float dot13(const float* a, const float* b) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 13; j++) s = fmaf(a[j], b[j], s);
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The fused per-instance solve.
+// ---------------------------------------------------------------------------------------------
+template <int W>
+__device__ void solve_instance(const float* __restrict__ rec, const KParams& P, Shared<W>& sh,
+                               float* __restrict__ fout, uint8_t* __restrict__ st_out,
+                               int32_t* __restrict__ it_out, int* __restrict__ ovf_list,
+                               int* __restrict__ ovf_count, int inst, float* __restrict__ Hout,
+                               float* __restrict__ gout) {
+  constexpr int NV = 64 * W;
+  constexpr int NT = 64 * W;
+  constexpr int LDM = Shared<W>::LDM;
+  const int v = threadIdx.x;           // reduced variable / row owned by this thread
+  const int lane = v & 63;
+  const int N = P.N;
+  const bool condense_only = (Hout != nullptr);
+
+  // ---- stance table: ub = gait * f_max, eliminated iff near_zero(ub) (SolverMPC.cpp:869-894)
+  const unsigned char* gait = reinterpret_cast<const unsigned char*>(rec + CMPC_REC_HDR + 12 * N);
+  for (int t = v; t < 4 * N; t += NT) {
+    const float ub = (float)gait[t] * P.f_max;
+    const bool elim = condense_only ? false : (ub < 0.01f && ub > -0.01f);
+    sh.stance[t] = elim ? 0 : 1;
+  }
+  for (int t = v; t < 12 * N; t += NT) sh.traj[t] = rec[CMPC_REC_HDR + t];
+  bsync<W>();
+  if (v < 64) {  // wave 0 compacts the stance foot steps
+    int base = 0;
+    for (int c0 = 0; c0 < 4 * N; c0 += 64) {
+      const int t = c0 + lane;
+      const bool f = (t < 4 * N) && sh.stance[t];
+      const unsigned long long m = __ballot(f);
+      const int pre = __popcll(m & ((1ull << lane) - 1ull));
+      if (f) {
+        sh.sfs[base + pre] = t;
+        sh.sub[base + pre] = (float)gait[t] * P.f_max;
+      }
+      base += __popcll(m);
+    }
+    if (lane == 0) sh.ctrl[0] = base;
+  }
+  bsync<W>();
+  const int nfs = sh.ctrl[0];
+  const int n = 3 * nfs;
+  if (n > NV && condense_only) return;
+  if (n > NV && ovf_list == nullptr) {  // no wider class available
+    for (int t = v; t < 12 * N; t += NT) fout[t] = 0.f;
+    if (v == 0) { st_out[0] = CMPC_BAD_INPUT; if (it_out) it_out[0] = 0; }
+    return;
+  }
+  if (n > NV) {  // needs a wider workgroup: hand the instance to the next size class
+    if (v == 0) {
+      const int slot = atomicAdd(ovf_count, 1);
+      ovf_list[slot] = inst;
+    }
+    return;
+  }
+  for (int t = v; t < NV; t += NT) {
+    if (t < n) {
+      const int fs = sh.sfs[t / 3];
+      sh.varblk[t] = (unsigned char)(fs >> 2);
+      sh.varcol[t] = (unsigned char)(3 * (fs & 3) + t % 3);
+    } else {
+      sh.varblk[t] = 0;
+      sh.varcol[t] = 0;
+    }
+  }
+  for (int i = v; i <= N; i += NT) {
+    int c = 0;
+    for (int s = 0; s < nfs; s++) c += (sh.sfs[s] < 4 * i) ? 1 : 0;
+    sh.blkbase[i] = 3 * c;
+  }
+  for (int t = v; t < 6 * nfs; t += NT) sh.cflag[t] = 0;
+
+  // ---- robot state (RobotState::set, quat_to_rpy) — uniform, computed by every thread
+  const float qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],
+              qz = rec[CMPC_REC_Q + 3];
+  Model md;
+  {
+    const float tx = 2.f * qx, ty = 2.f * qy, tz = 2.f * qz;
+    const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    md.R[0] = 1.f - (tyy + tzz); md.R[1] = txy - twz;         md.R[2] = txz + twy;
+    md.R[3] = txy + twz;         md.R[4] = 1.f - (txx + tzz); md.R[5] = tyz - twx;
+    md.R[6] = txz - twy;         md.R[7] = tyz + twx;         md.R[8] = 1.f - (txx + tyy);
+  }
+  md.dt = P.dt;
+  md.dth = P.dt * P.dt * 0.5f;
+  md.xdrag = rec[CMPC_REC_XDRAG];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) md.n1r[i * 3 + j] = P.dt * md.R[j * 3 + i];
+
+  // Bdt columns -> LDS (thread t computes entry (s = t % 13, c = t / 13))
+  {
+    // I_world = R diag(Ib) R^T, I_inv (SolverMPC.cpp:593, 273)
+    const float Ib[3] = {.07f, 0.26f, 0.242f};
+    float Iw[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+        Iw[i * 3 + j] = md.R[i * 3 + 0] * Ib[0] * md.R[j * 3 + 0] + md.R[i * 3 + 1] * Ib[1] * md.R[j * 3 + 1] +
+                        md.R[i * 3 + 2] * Ib[2] * md.R[j * 3 + 2];
+    const float c00 = Iw[4] * Iw[8] - Iw[5] * Iw[7];
+    const float c10 = Iw[5] * Iw[6] - Iw[3] * Iw[8];
+    const float c20 = Iw[3] * Iw[7] - Iw[4] * Iw[6];
+    const float idet = 1.f / (Iw[0] * c00 + Iw[1] * c10 + Iw[2] * c20);
+    float Ii[9];
+    Ii[0] = c00 * idet; Ii[1] = (Iw[2] * Iw[7] - Iw[1] * Iw[8]) * idet; Ii[2] = (Iw[1] * Iw[5] - Iw[2] * Iw[4]) * idet;
+    Ii[3] = c10 * idet; Ii[4] = (Iw[0] * Iw[8] - Iw[2] * Iw[6]) * idet; Ii[5] = (Iw[2] * Iw[3] - Iw[0] * Iw[5]) * idet;
+    Ii[6] = c20 * idet; Ii[7] = (Iw[1] * Iw[6] - Iw[0] * Iw[7]) * idet; Ii[8] = (Iw[0] * Iw[4] - Iw[1] * Iw[3]) * idet;
+    const float im = 1.f / 12.0f;  // RobotState.h:26
+    const float dt = P.dt, dt2 = md.dth, dt3 = P.dt * P.dt * P.dt / 6.f;
+    for (int t = v; t < 13 * 12; t += NT) {
+      const int s = t % 13, c = t / 13;
+      const int b = c / 3, a = c % 3;
+      const float r0 = rec[CMPC_REC_R + 0 * 4 + b], r1 = rec[CMPC_REC_R + 1 * 4 + b], r2 = rec[CMPC_REC_R + 2 * 4 + b];
+      // column a of [r]x : ([r]x)[k][a]
+      float cx[3];
+      if (a == 0) { cx[0] = 0.f; cx[1] = r2; cx[2] = -r1; }
+      else if (a == 1) { cx[0] = -r2; cx[1] = 0.f; cx[2] = r0; }
+      else { cx[0] = r1; cx[1] = -r0; cx[2] = 0.f; }
+      float T[3];  // B_c[6+i][c] = (I_inv [r]x)[i][a]
+#pragma unroll
+      for (int i = 0; i < 3; i++) T[i] = Ii[i * 3 + 0] * cx[0] + Ii[i * 3 + 1] * cx[1] + Ii[i * 3 + 2] * cx[2];
+      const float b9 = (a == 0) ? im : 0.f;  // B_c[9][c]
+      float val = 0.f;
+      if (s < 3) {
+        // (R^T T)[s] with a register-only select on s (no runtime-indexed arrays -> no scratch)
+        const float c0 = (s == 0) ? md.R[0] : (s == 1) ? md.R[1] : md.R[2];
+        const float c1 = (s == 0) ? md.R[3] : (s == 1) ? md.R[4] : md.R[5];
+        const float c2 = (s == 0) ? md.R[6] : (s == 1) ? md.R[7] : md.R[8];
+        val = dt2 * (c0 * T[0] + c1 * T[1] + c2 * T[2]);
+      } else if (s < 6) {
+        val = dt2 * (((s - 3) == a) ? im : 0.f);
+        if (s == 5) val += dt3 * md.xdrag * b9;
+      } else if (s < 9) {
+        val = dt * ((s == 6) ? T[0] : (s == 7) ? T[1] : T[2]);
+      } else if (s < 12) {
+        val = dt * (((s - 9) == a) ? im : 0.f);
+        if (s == 11) val += dt2 * md.xdrag * b9;
+      }
+      sh.BdtT[c][s] = val;
+    }
+    for (int t = v; t < 12 * 3; t += NT) sh.BdtT[t / 3][13 + t % 3] = 0.f;
+  }
+  // e_i = Adt^{i+1} x0 + sum_{k<=i} Adt^k Qdt f - X_d,i  for each step i (thread i), into LDS.
+  // Adt^m = I + m N1 + m(m-1)/2 N1^2 exactly (N1^3 = 0).
+  if (v < N) {
+    float x0[13];
+    {
+    float as = -2.f * (qx * qz - qw * qy);
+    as = fminf(as, 0.99999f);
+    const float yaw = atan2f(2.f * (qx * qy + qw * qz), qw * qw + qx * qx - qy * qy - qz * qz);
+    const float pitch = asinf(as);
+    const float roll = atan2f(2.f * (qy * qz + qw * qx), qw * qw - qx * qx - qy * qy + qz * qz);
+    x0[0] = roll; x0[1] = pitch; x0[2] = yaw;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      x0[3 + i] = rec[CMPC_REC_P + i];
+      x0[6 + i] = rec[CMPC_REC_W + i];
+      x0[9 + i] = rec[CMPC_REC_V + i];
+    }
+    x0[12] = -9.8f;
+  }
+
+    float X1[13], X2[13], qf[13], F1[13], F2[13];
+    n1_mul(md, x0, X1);
+    n1_mul(md, X1, X2);
+    // Q_qp f with f = (0,0,0,f_est(3),0,0) when the history flag is set (SolverMPC.cpp:808-811)
+    const uint32_t flags = __float_as_uint(rec[CMPC_REC_FLAGS]);
+    const float f3 = (flags & 1u) ? rec[CMPC_REC_FEST3] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 13; j++) qf[j] = 0.f;
+    // Qdt[:,3] = dt e9 + dt^2/2 (e3 + xdrag e11) + dt^3/6 xdrag e5
+    qf[9] = P.dt * f3;
+    qf[3] = md.dth * f3;
+    qf[11] = md.dth * md.xdrag * f3;
+    qf[5] = (P.dt * P.dt * P.dt / 6.f) * md.xdrag * f3;
+    n1_mul(md, qf, F1);
+    n1_mul(md, F1, F2);
+    const int i = v;
+    const float m1 = (float)(i + 1);
+    const float m2 = 0.5f * m1 * (float)i;
+    const float s2 = 0.5f * (float)i * (float)(i + 1);
+    const float s3 = (float)(i + 1) * (float)i * (float)(i - 1) / 6.f;
+#pragma unroll
+    for (int j = 0; j < 13; j++) {
+      float e = x0[j] + m1 * X1[j] + m2 * X2[j] + m1 * qf[j] + s2 * F1[j] + s3 * F2[j];
+      if (j < 12) e -= sh.traj[i * 12 + j];
+      sh.E[i][j] = e;
+    }
+  }
+  bsync<W>();
+  // gradient recursion ze_i = S e_i + Adt' ze_{i+1} (uniform; wave 0 computes, lane 0 stores)
+  if (v < 64) {
+    float wts[13];
+#pragma unroll
+    for (int j = 0; j < 12; j++) wts[j] = P.wts[j];
+    wts[12] = 0.f;
+    float ze[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) ze[j] = 0.f;
+    for (int i = N - 1; i >= 0; i--) {
+      float e[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) e[j] = sh.E[i][j];
+      recur(md, wts, e, ze);
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < 13; j++) sh.ZE[i][j] = ze[j];
+      }
+    }
+  }
+  bsync<W>();
+
+  // ---- condensation: thread v fills its row of the (reduced) Hessian + gradient ------------
+  float slot[NV + 1];
+#pragma unroll
+  for (int c = 0; c <= NV; c++) slot[c] = (c == v && v >= n) ? 1.f : 0.f;  // identity padding
+  {
+    float wts[13];
+#pragma unroll
+    for (int j = 0; j < 12; j++) wts[j] = P.wts[j];
+    wts[12] = 0.f;
+    const bool real = v < n;
+    const int kv = real ? sh.varblk[v] : 0;
+    const int cv = real ? sh.varcol[v] : 0;
+    float b[13], u1[13], u2[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) b[j] = real ? sh.BdtT[cv][j] : 0.f;
+    n1_mul(md, b, u1);
+    n1_mul(md, u1, u2);
+    float gv = 0.f;
+    {
+      float zk[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) zk[j] = sh.ZE[kv][j];
+      gv = 2.f * dot13(b, zk);
+    }
+    float z[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) z[j] = 0.f;
+    for (int i = N - 1; i >= 0; i--) {
+      {
+        const float k = (float)(i - kv);
+        const float k2 = 0.5f * k * (k - 1.f);
+        float gk[13];
+#pragma unroll
+        for (int j = 0; j < 13; j++) gk[j] = b[j] + k * u1[j] + k2 * u2[j];
+        recur(md, wts, gk, z);
+      }
+      const int base = __builtin_amdgcn_readfirstlane(sh.blkbase[i]);
+      const int end = __builtin_amdgcn_readfirstlane(sh.blkbase[i + 1]);
+#pragma unroll
+      for (int w = 0; w < NV; w++) {
+        if (w >= base && w < end) {
+          const int cw = sh.varcol[w];
+          float bw[13];
+#pragma unroll
+          for (int j = 0; j < 13; j++) bw[j] = sh.BdtT[cw][j];
+          float val = 2.f * dot13(bw, z);
+          if (w == v) val += P.alpha2;
+          slot[w] = real ? val : slot[w];
+        }
+      }
+    }
+    slot[NV] = real ? gv : 0.f;
+  }
+
+  if (condense_only) {  // parity hook: write the (full, nothing eliminated) qH row and qg
+    const int nv_full = 12 * N;
+    if (v < n) {
+#pragma unroll
+      for (int w = 0; w < NV; w++)
+        if (w < n) {
+          // variables are never eliminated here, so v == 12 k + c ordering holds
+          const bool upper = sh.varblk[w] > sh.varblk[v] || (sh.varblk[w] == sh.varblk[v] && w >= v);
+          if (upper) {
+            Hout[(size_t)v * nv_full + w] = slot[w];
+            Hout[(size_t)w * nv_full + v] = slot[w];
+          }
+        }
+      gout[v] = slot[NV];
+    }
+    return;
+  }
+
+  // ---- bordered Cholesky H = U'U, [U | y] with U' y = g (rows in registers, raw rows in M) --
+  int status = CMPC_OK;
+  float my_inv = 1.f;
+  for (int k = 0; k < n; k++) {
+    float* Mk = &sh.M[k * LDM];
+    if (v == k) {
+#pragma unroll
+      for (int c = 0; c < NV; c += 4)
+        *reinterpret_cast<float4*>(&Mk[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
+      Mk[NV] = slot[NV];
+    }
+    bsync<W>();
+    float d2 = Mk[k];
+    if (!(d2 > 0.f)) { status = CMPC_NOT_PD; d2 = 1e-30f; }
+    const float inv = rsqrtf(d2);
+    if (v == k) my_inv = inv;
+    const float a = (v > k) ? -Mk[v] * inv * inv : 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; c += 4) {
+      const float4 r4 = *reinterpret_cast<const float4*>(&Mk[c]);
+      slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
+      slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
+      slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
+      slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+    }
+    slot[NV] = fmaf(a, Mk[NV], slot[NV]);
+  }
+  // y_v = raw border * inv_v ; U row v = raw row * inv_v (in M, scaled on read)
+  const float yv = slot[NV] * my_inv;
+
+  // ---- J = U^{-1}, rows in registers (acc[v] = -1 on the diagonal) --------
+#pragma unroll
+  for (int c = 0; c < NV; c++) slot[c] = (c == v) ? -1.f : 0.f;
+  for (int l = n - 1; l >= 0; l--) {
+    float* bx = sh.bufA[l & 1];
+    if (v == l) {
+#pragma unroll
+      for (int c = 0; c < NV; c += 4)
+        *reinterpret_cast<float4*>(&bx[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
+    }
+    bsync<W>();
+    const float inv_l = rsqrtf(sh.M[l * LDM + l]);
+    const float a = (v < l) ? -(sh.M[v * LDM + l] * my_inv) * inv_l : 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; c += 4) {
+      const float4 r4 = *reinterpret_cast<const float4*>(&bx[c]);
+      slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
+      slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
+      slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
+      slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+    }
+  }
+  {
+    const float s = -my_inv;
+#pragma unroll
+    for (int c = 0; c < NV; c++) slot[c] *= s;
+  }
+
+  // ---- unconstrained minimiser x = -U^{-1} y ----------------------------------------------
+  sh.dfull[v] = yv;
+  bsync<W>();
+  float xv = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; c += 4) {
+    const float4 y4 = *reinterpret_cast<const float4*>(&sh.dfull[c]);
+    xv = fmaf(slot[c + 0], y4.x, xv);
+    xv = fmaf(slot[c + 1], y4.y, xv);
+    xv = fmaf(slot[c + 2], y4.z, xv);
+    xv = fmaf(slot[c + 3], y4.w, xv);
+  }
+  xv = -xv;
+  if (v >= n) xv = 0.f;
+  bsync<W>();
+
+  // ---- Goldfarb-Idnani dual active set on the friction pyramids ---------------------------
+  // constraint id c = 6 s + t for stance foot step s (reduced vars 3s, 3s+1, 3s+2):
+  //   t=0..3: +-fx/mu + fz >= 0, +-fy/mu + fz >= 0 ; t=4: fz >= 0 ; t=5: -fz >= -ub
+  const float mui = P.mu_inv;
+  const float fnorm = 1.f / sqrtf(mui * mui + 1.f);
+  int q = 0;
+  int iters = 0;
+  const int cap = P.max_iter;
+  if (status == CMPC_OK) {
+    for (;;) {
+      sh.xs[v] = xv;
+      bsync<W>();
+      // most violated constraint (normalised slack)
+      float best = 0.f;
+      int bid = 0x7fffffff;
+      for (int s = v; s < nfs; s += NT) {
+        const float fx = sh.xs[3 * s], fy = sh.xs[3 * s + 1], fz = sh.xs[3 * s + 2];
+        float sl[6];
+        sl[0] = (mui * fx + fz) * fnorm;
+        sl[1] = (-mui * fx + fz) * fnorm;
+        sl[2] = (mui * fy + fz) * fnorm;
+        sl[3] = (-mui * fy + fz) * fnorm;
+        sl[4] = fz;
+        sl[5] = sh.sub[s] - fz;
+#pragma unroll
+        for (int t = 0; t < 6; t++)
+          if (!sh.cflag[6 * s + t] && sl[t] < best) { best = sl[t]; bid = 6 * s + t; }
+      }
+      float xmax = block_max<W>(fabsf(xv), sh);
+      block_argmin<W>(best, bid, sh);
+      const float tol = 1e-5f * fmaxf(1.f, xmax);
+      if (bid == 0x7fffffff || best >= -tol) break;
+
+      const int p = bid;
+      const int sp_ = p / 6, tp = p % 6;
+      const int iz = 3 * sp_ + 2;
+      int ia;
+      float ca, cb, bp;
+      if (tp < 4) {
+        ia = 3 * sp_ + (tp >> 1);
+        ca = (tp & 1) ? -mui : mui;
+        cb = 1.f;
+        bp = 0.f;
+      } else if (tp == 4) {
+        ia = iz; ca = 0.f; cb = 1.f; bp = 0.f;
+      } else {
+        ia = iz; ca = 0.f; cb = -1.f; bp = -sh.sub[sp_];
+      }
+      float up = 0.f;
+      bool added = false;
+      while (!added) {
+        if (++iters > cap) { status = CMPC_MAX_ITER; break; }
+        // d = J' n+
+        if (v == ia) {
+#pragma unroll
+          for (int c = 0; c < NV; c += 4)
+            *reinterpret_cast<float4*>(&sh.bufA[0][c]) =
+                make_float4(ca * slot[c], ca * slot[c + 1], ca * slot[c + 2], ca * slot[c + 3]);
+        }
+        bsync<W>();
+        if (v == iz) {
+#pragma unroll
+          for (int c = 0; c < NV; c += 4) {
+            float4 a4 = *reinterpret_cast<const float4*>(&sh.bufA[0][c]);
+            if (ia == iz) a4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(&sh.bufB[c]) =
+                make_float4(fmaf(cb, slot[c], a4.x), fmaf(cb, slot[c + 1], a4.y),
+                            fmaf(cb, slot[c + 2], a4.z), fmaf(cb, slot[c + 3], a4.w));
+          }
+        }
+        bsync<W>();
+        const float dv = sh.bufB[v];
+        sh.dfull[v] = dv;
+        sh.dmask[v] = (v >= q) ? dv : 0.f;
+        bsync<W>();
+        // z = J2 d2 ; zn = |d2|^2 ; dn = |d|^2
+        float zv = 0.f, zn = 0.f, dn = 0.f;
+#pragma unroll
+        for (int c = 0; c < NV; c += 4) {
+          const float4 m4 = *reinterpret_cast<const float4*>(&sh.dmask[c]);
+          const float4 f4 = *reinterpret_cast<const float4*>(&sh.dfull[c]);
+          zv = fmaf(slot[c + 0], m4.x, zv);
+          zv = fmaf(slot[c + 1], m4.y, zv);
+          zv = fmaf(slot[c + 2], m4.z, zv);
+          zv = fmaf(slot[c + 3], m4.w, zv);
+          zn += m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
+          dn += f4.x * f4.x + f4.y * f4.y + f4.z * f4.z + f4.w * f4.w;
+        }
+        // r = R^{-1} d1 (back substitution, R upper triangular q x q in M)
+        float rr = dv;
+        for (int l = q - 1; l >= 0; l--) {
+          if (v == l) sh.rvec[l] = rr / sh.M[l * LDM + l];
+          bsync<W>();
+          const float rl = sh.rvec[l];
+          if (v < l) rr = fmaf(-sh.M[v * LDM + l], rl, rr);
+        }
+        // t1: partial (dual) step
+        float t1 = kBigF;
+        int kk = 0x7fffffff;
+        if (v < q) {
+          const float rj = sh.rvec[v];
+          if (rj > 0.f) { t1 = fmaxf(sh.u[v] / rj, 0.f); kk = v; }
+        }
+        block_argmin<W>(t1, kk, sh);
+        // t2: full (primal) step
+        const float spv = fmaf(ca, sh.xs[ia], fmaf(cb, sh.xs[iz], -bp));  // ca = 0 when ia == iz
+        const bool zero_step = !(zn > 1e-9f * dn);
+        const float t2 = zero_step ? kBigF : -spv / zn;
+        const float t = fminf(t1, t2);
+        if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
+        if (v < q) sh.u[v] = fmaf(-t, sh.rvec[v], sh.u[v]);
+        up += t;
+        if (!zero_step) {
+          xv = fmaf(t, zv, xv);
+          sh.xs[v] = xv;
+        }
+        bsync<W>();
+        if (!zero_step && t2 <= t1) {
+          // ---- add p: Givens rotations zeroing d[q+1..n-1] into d[q] (suffix norms) ----
+          const float dsq = (v >= q && v < n) ? dv * dv : 0.f;
+          const float ts = sqrtf(block_suffix_sum<W>(dsq, sh));
+          sh.tsv[v] = ts;
+          bsync<W>();
+          if (v > q && v < n) {
+            const float h = sh.tsv[v - 1];
+            const float cur = (v == n - 1) ? dv : ts;
+            const float dprev = sh.dfull[v - 1];
+            float c_ = 1.f, s_ = 0.f;
+            if (h > 0.f) { c_ = dprev / h; s_ = cur / h; }
+            sh.cs[2 * v] = c_;
+            sh.cs[2 * v + 1] = s_;
+          }
+          // new R column q
+          if (v < q) sh.M[v * LDM + q] = dv;
+          if (v == q) {
+            sh.M[q * LDM + q] = (q == n - 1) ? dv : ts;  // no rotation when q = n-1
+            sh.act[q] = p;
+            sh.u[q] = up;
+            sh.cflag[p] = 1;
+          }
+          bsync<W>();
+#pragma unroll
+          for (int j = NV - 1; j >= 1; j--) {
+            if (j > q && j < n) {
+              const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+              const float a0 = slot[j - 1], b0 = slot[j];
+              slot[j - 1] = fmaf(cs2.x, a0, cs2.y * b0);
+              slot[j] = fmaf(-cs2.y, a0, cs2.x * b0);
+            }
+          }
+          q++;
+          added = true;
+        } else {
+          // ---- drop constraint kk ----
+          const int k = kk;
+          // shift act/u left over [k, q-2]
+          int a_next = 0;
+          float u_next = 0.f;
+          if (v >= k && v < q - 1) { a_next = sh.act[v + 1]; u_next = sh.u[v + 1]; }
+          if (v == k) sh.cflag[sh.act[k]] = 0;
+          bsync<W>();
+          if (v >= k && v < q - 1) { sh.act[v] = a_next; sh.u[v] = u_next; }
+          // remove column k of R: each row owner shifts its row
+          if (v < q) {
+            float* Rv = &sh.M[v * LDM];
+            for (int c = k; c < q - 1; c++) Rv[c] = Rv[c + 1];
+          }
+          bsync<W>();
+          // re-triangularise rows j, j+1 (j = k..q-2), collecting the rotations
+          for (int j = k; j < q - 1; j++) {
+            const float a0 = sh.M[j * LDM + j], b0 = sh.M[(j + 1) * LDM + j];
+            const float h = sqrtf(a0 * a0 + b0 * b0);
+            float c_ = 1.f, s_ = 0.f;
+            if (h > 0.f) { c_ = a0 / h; s_ = b0 / h; }
+            bsync<W>();
+            if (v >= j && v < q - 1) {
+              const float rj = sh.M[j * LDM + v], rj1 = sh.M[(j + 1) * LDM + v];
+              sh.M[j * LDM + v] = fmaf(c_, rj, s_ * rj1);
+              sh.M[(j + 1) * LDM + v] = fmaf(-s_, rj, c_ * rj1);
+            }
+            if (v == 0) { sh.cs[2 * j] = c_; sh.cs[2 * j + 1] = s_; }
+            bsync<W>();
+          }
+          // same rotations on J columns (j, j+1)
+#pragma unroll
+          for (int j = 0; j < NV - 1; j++) {
+            if (j >= k && j < q - 1) {
+              const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+              const float a0 = slot[j], b0 = slot[j + 1];
+              slot[j] = fmaf(cs2.x, a0, cs2.y * b0);
+              slot[j + 1] = fmaf(-cs2.y, a0, cs2.x * b0);
+            }
+          }
+          q--;
+        }
+        bsync<W>();
+      }
+      if (status != CMPC_OK) break;
+    }
+  }
+
+  // ---- scatter forces (q_soln layout: 12 k + 3 leg + axis; swing -> 0) --------------------
+  const bool ok = (status == CMPC_OK);
+  if (v < n) {
+    const int kv = sh.varblk[v], cv = sh.varcol[v];
+    fout[12 * kv + cv] = ok ? xv : 0.f;
+  }
+  for (int t = v; t < 12 * N; t += NT)
+    if (!sh.stance[t / 3] || !ok) fout[t] = 0.f;
+  if (v == 0) {
+    st_out[0] = (uint8_t)status;
+    if (it_out) it_out[0] = iters;
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// Kernels. The first size class runs one workgroup per instance over the whole batch; larger
+// classes run a persistent grid over the overflow list filled by the previous class.
+// ---------------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(64 * W) void cmpc_solve_kernel(
+    const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
+    uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
+    const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
+  __shared__ Shared<W> sh;
+  const int count = in_list ? *in_count : batch;
+  for (int t = blockIdx.x; t < count; t += gridDim.x) {
+    const int inst = in_list ? in_list[t] : t;
+    solve_instance<W>(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
+                      status + inst, iters ? iters + inst : nullptr, ovf_list, ovf_count, inst,
+                      nullptr, nullptr);
+    __syncthreads();
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W) void cmpc_condense_kernel(const float* __restrict__ recs,
+                                                               int batch, KParams P,
+                                                               float* __restrict__ H,
+                                                               float* __restrict__ g) {
+  __shared__ Shared<W> sh;
+  const int nv = 12 * P.N;
+  for (int inst = blockIdx.x; inst < batch; inst += gridDim.x) {
+    solve_instance<W>(recs + (size_t)inst * P.rec_words, P, sh, nullptr, nullptr, nullptr, nullptr,
+                      nullptr, inst, H + (size_t)inst * nv * nv, g + (size_t)inst * nv);
+    __syncthreads();
+  }
+}
+
+hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
+                        uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
+                        hipStream_t stream, hipEvent_t* ev) {
+  // d_work layout: [0] overflow count of class 1, [1] of class 2, [4 ..) lists [max_batch] x 2
+  int* cnt1 = d_work;
+  int* list1 = d_work + 4;
+  hipError_t e = hipMemsetAsync(d_work, 0, 4 * sizeof(int), stream);
+  if (e != hipSuccess) return e;
+  if (batch <= 0) return hipSuccess;
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  // class 1: one 64-thread workgroup per instance; instances with > 64 stance variables are
+  // appended to list1
+  hipLaunchKernelGGL(cmpc_solve_kernel<1>, dim3(batch), dim3(64), 0, stream, d_recs, batch, P,
+                     d_forces, d_status, d_iters, nullptr, nullptr, list1, cnt1);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (ev) (void)hipEventRecord(ev[1], stream);
+  if (12 * P.N > 64) {
+    // class 2: persistent grid of 128-thread workgroups over list1
+    const int g2 = batch < 2048 ? batch : 2048;
+    hipLaunchKernelGGL(cmpc_solve_kernel<2>, dim3(g2), dim3(128), 0, stream, d_recs, batch, P,
+                       d_forces, d_status, d_iters, list1, cnt1, nullptr, nullptr);
+    e = hipGetLastError();
+  }
+  if (ev) (void)hipEventRecord(ev[2], stream);
+  return e;
+}
+
+hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
+                           hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  const int nv = 12 * P.N;
+  if (nv <= 64)
+    hipLaunchKernelGGL(cmpc_condense_kernel<1>, dim3(batch), dim3(64), 0, stream, d_recs, batch, P, d_H, d_g);
+  else if (nv <= 128)
+    hipLaunchKernelGGL(cmpc_condense_kernel<2>, dim3(batch), dim3(128), 0, stream, d_recs, batch, P, d_H, d_g);
+  else
+    return hipErrorInvalidValue;  // 12N > 128 needs the 4-wave class (not built yet)
+  return hipGetLastError();
+}
+
+}  // namespace cmpc

@@ -1,0 +1,103 @@
+"""Synthetic batched MPC instances (SURVEY.md §8(d) generator).
+
+Each instance is one ``solveDenseMPC`` call of a Unitree A1 in trot
+(``ConvexMPCLocomotion.cpp:612-870``): a randomised body state, foot offsets around the A1
+nominal stance, a trot contact table at a random phase (``Gait.cpp:159-188``,
+``OffsetDurationGait`` with P = 18, offsets (0, 9, 9, 0), durations 9:
+``ConvexMPCLocomotion.cpp:41``), and the reference trajectory ``trajAll`` built exactly as
+``updateMPCIfNeeded`` does (``ConvexMPCLocomotion.cpp:554-585``). A fraction of instances get
+Bernoulli(0.5) contacts instead (stress / ragged reduced sizes).
+
+Deterministic: numpy ``Generator(Philox(seed))``, fully vectorised.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .records import pack_records
+
+BASE_SEED = 20251015
+# A1 hip offsets (MiniCheetah-style leg order FR, FL, RR, RL): x = +-0.1805, y = -+0.047,
+# plus the abad link +-0.0838 in y (common/Dynamics/MiniCheetah.h:27-40, Quadruped.h:95-102).
+_HIP_X = np.array([0.1805, 0.1805, -0.1805, -0.1805])
+_HIP_Y = np.array([-0.047, 0.047, -0.047, 0.047]) + np.array([-0.0838, 0.0838, -0.0838, 0.0838])
+
+
+def trot_table(horizon: int, iteration: np.ndarray, period: int = 18) -> np.ndarray:
+    """OffsetDurationGait::getMpcTable (Gait.cpp:159-188) for the trot gait; rows i < N.
+
+    For N > P the reference would read past its P-row table; the period is stretched to N
+    there."""
+    P = max(period, horizon)
+    offsets = np.array([0, P // 2, P // 2, 0])
+    durations = np.array([P // 2] * 4)
+    i = np.arange(horizon)[None, :, None]
+    it = (i + iteration[:, None, None] + 1) % P
+    prog = it - offsets[None, None, :]
+    prog = np.where(prog < 0, prog + P, prog)
+    return (prog < durations[None, None, :]).astype(np.int32).reshape(iteration.shape[0], 4 * horizon)
+
+
+def euler_zyx_to_quat(roll, pitch, yaw):
+    cr, sr = np.cos(roll / 2), np.sin(roll / 2)
+    cp, sp = np.cos(pitch / 2), np.sin(pitch / 2)
+    cy, sy = np.cos(yaw / 2), np.sin(yaw / 2)
+    w = cr * cp * cy + sr * sp * sy
+    x = sr * cp * cy - cr * sp * sy
+    y = cr * sp * cy + sr * cp * sy
+    z = cr * cp * sy - sr * sp * cy
+    return np.stack([w, x, y, z], axis=-1)
+
+
+def make_instances(batch: int, horizon: int = 10, seed: int = BASE_SEED, dt: float = 0.026,
+                   random_contact_frac: float = 0.25, body_height: float = 0.29,
+                   x_drag_range: float = 0.5, stress: bool = False) -> np.ndarray:
+    """Return packed records [batch, record_words(horizon)] (float32).
+
+    ``stress`` widens the velocity/orientation errors so friction cones bind (active sets)."""
+    g = np.random.Generator(np.random.Philox(seed))
+    B, N = batch, horizon
+    scale = 3.0 if stress else 1.0
+    roll = np.clip(g.normal(0, 0.05 * scale, B), -0.3 * scale, 0.3 * scale)
+    pitch = np.clip(g.normal(0, 0.05 * scale, B), -0.3 * scale, 0.3 * scale)
+    yaw = g.uniform(-np.pi, np.pi, B)
+    q = euler_zyx_to_quat(roll, pitch, yaw)
+    p = np.stack([g.uniform(-1, 1, B), g.uniform(-1, 1, B), body_height + g.normal(0, 0.02, B)], -1)
+    v = np.stack([g.uniform(-0.7, 0.7, B) * scale, g.uniform(-0.4, 0.4, B) * scale,
+                  g.normal(0, 0.05, B)], -1)
+    w = g.normal(0, 0.3 * scale, (B, 3))
+    # foot offsets r = pFoot - p in world frame (axis-major, ConvexMPCLocomotion.cpp:786-790)
+    cy, sy = np.cos(yaw)[:, None], np.sin(yaw)[:, None]
+    bx = _HIP_X[None, :] + g.normal(0, 0.03, (B, 4))
+    by = _HIP_Y[None, :] + g.normal(0, 0.03, (B, 4))
+    rx = cy * bx - sy * by
+    ry = sy * bx + cy * by
+    rz = -p[:, 2:3] + g.normal(0, 0.02, (B, 4))
+    r = np.concatenate([rx, ry, rz], axis=1)
+    # contact table: trot at a random phase; a fraction with Bernoulli(0.5) contacts
+    gait = trot_table(N, g.integers(0, 18, B))
+    rnd = g.random(B) < random_contact_frac
+    if rnd.any():
+        gait[rnd] = (g.random((int(rnd.sum()), 4 * N)) < 0.5).astype(np.int32)
+    # trajectory (ConvexMPCLocomotion.cpp:554-585)
+    vdes_x = g.uniform(-0.7, 0.7, B) * scale
+    vdes_y = g.uniform(-0.4, 0.4, B) * scale
+    yaw_rate = g.uniform(-2.5, 2.5, B)
+    x_start = p[:, 0] + g.uniform(-0.1, 0.1, B)
+    y_start = p[:, 1] + g.uniform(-0.1, 0.1, B)
+    traj = np.zeros((B, N, 12), np.float32)
+    traj[:, :, 2] = (yaw + g.normal(0, 0.05, B))[:, None]   # _yaw_des
+    traj[:, :, 3] = x_start[:, None]
+    traj[:, :, 4] = y_start[:, None]
+    traj[:, :, 5] = body_height
+    traj[:, :, 8] = yaw_rate[:, None]
+    traj[:, :, 9] = vdes_x[:, None]
+    traj[:, :, 10] = vdes_y[:, None]
+    traj[:, 0, 2] = yaw                                  # trajAll[2] = seResult.rpy[2]
+    for i in range(1, N):                                # fp32 recurrence as the caller
+        traj[:, i, 3] = traj[:, i - 1, 3] + np.float32(dt) * traj[:, i, 9]
+        traj[:, i, 4] = traj[:, i - 1, 4] + np.float32(dt) * traj[:, i, 10]
+        traj[:, i, 2] = traj[:, i - 1, 2] + np.float32(dt) * traj[:, i, 8]
+    x_drag = g.uniform(-x_drag_range, x_drag_range, B)
+    rpy = np.stack([roll, pitch, yaw], -1)
+    return pack_records(p, v, q, w, r, traj.reshape(B, 12 * N), gait, rpy=rpy, x_drag=x_drag)

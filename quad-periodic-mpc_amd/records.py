@@ -1,0 +1,112 @@
+"""Instance-record layout shared by the HIP solver, the C ABI and the oracle.
+
+One record holds one ``solve_mpc`` call's per-instance data (reference:
+``be2r_cmpc_unitree/src/controllers/convexMPC/SolverMPC.cpp:566-655``, the fields of
+``update_data_t`` in ``convexMPC_interface.h:23-41``). The word offsets mirror the ``CMPC_REC_*``
+macros of ``include/cmpc_solver.h``; keep the two in sync.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+REC_P = 0        # p[3]
+REC_V = 3        # v[3]
+REC_Q = 6        # q[4] (w, x, y, z)
+REC_W = 10       # omega[3]
+REC_R = 13       # r[12] axis-major 3x4: r[axis * 4 + leg]
+REC_RPY = 25     # roll, pitch, yaw (stored; the solve recomputes rpy from q)
+REC_XDRAG = 28   # x_drag
+REC_FEST3 = 29   # f_est(3) compensation force (config 5)
+REC_FLAGS = 30   # uint32 bit-cast; bit 0: use f_est in qg
+REC_HDR = 32
+MAX_HORIZON = 24
+
+STATUS_NAMES = {0: "ok", 1: "max_iter", 2: "infeasible", 3: "not_pd", 4: "bad_input"}
+
+
+def record_words(horizon: int) -> int:
+    """fp32 words per record: header + traj[12N] + gait[4N] bytes, padded to 16 B."""
+    return (REC_HDR + 13 * horizon + 3) & ~3
+
+
+def traj_offset(horizon: int) -> int:
+    return REC_HDR
+
+
+def gait_offset(horizon: int) -> int:
+    return REC_HDR + 12 * horizon
+
+
+class CmpcParams(ctypes.Structure):
+    """ctypes mirror of ``cmpc_params`` (include/cmpc_solver.h)."""
+
+    _fields_ = [
+        ("dt", ctypes.c_float),
+        ("mu", ctypes.c_float),
+        ("f_max", ctypes.c_float),
+        ("horizon", ctypes.c_int),
+        ("weights", ctypes.c_float * 12),
+        ("alpha", ctypes.c_float),
+        ("max_iter", ctypes.c_int),
+    ]
+
+
+# ConvexMPCLocomotion.cpp:617 (Q), :623 (alpha), :807 (mu = 0.4, f_max = 120); dtMPC = 0.002 * 13
+DEFAULT_WEIGHTS = (0.25, 0.25, 10, 10, 2, 50, 0, 0, 0.3, 0.2, 0.2, 0.1)
+
+
+def make_params(horizon: int = 10, dt: float = 0.026, mu: float = 0.4, f_max: float = 120.0,
+                weights=DEFAULT_WEIGHTS, alpha: float = 4e-5, max_iter: int = 100) -> CmpcParams:
+    if not 1 <= horizon <= MAX_HORIZON:
+        raise ValueError(f"horizon {horizon} outside 1..{MAX_HORIZON}")
+    prm = CmpcParams()
+    prm.dt = dt
+    prm.mu = mu
+    prm.f_max = f_max
+    prm.horizon = horizon
+    for i, w in enumerate(weights):
+        prm.weights[i] = w
+    prm.alpha = alpha
+    prm.max_iter = max_iter
+    return prm
+
+
+def pack_records(p, v, q, w, r, traj, gait, *, rpy=None, x_drag=None, f_est3=None,
+                 use_f_est=None) -> np.ndarray:
+    """Pack per-instance arrays (leading batch dim) into a [B, record_words(N)] fp32 array.
+
+    ``r`` is axis-major [B, 12] (``r[axis*4 + leg]``, ConvexMPCLocomotion.cpp:786-790),
+    ``traj`` [B, 12N] step-major, ``gait`` [B, 4N] integers cast to uint8 as
+    ``convexMPC_interface.cpp:139`` does.
+    """
+    p = np.asarray(p, np.float32)
+    B = p.shape[0]
+    traj = np.asarray(traj, np.float32).reshape(B, -1)
+    N = traj.shape[1] // 12
+    gait = np.asarray(gait).reshape(B, 4 * N).astype(np.uint8)
+    rec = np.zeros((B, record_words(N)), np.float32)
+    rec[:, REC_P:REC_P + 3] = p
+    rec[:, REC_V:REC_V + 3] = v
+    rec[:, REC_Q:REC_Q + 4] = q
+    rec[:, REC_W:REC_W + 3] = w
+    rec[:, REC_R:REC_R + 12] = r
+    if rpy is not None:
+        rec[:, REC_RPY:REC_RPY + 3] = rpy
+    if x_drag is not None:
+        rec[:, REC_XDRAG] = x_drag
+    if f_est3 is not None:
+        rec[:, REC_FEST3] = f_est3
+    if use_f_est is not None:
+        rec[:, REC_FLAGS] = np.asarray(use_f_est, np.uint32).astype(np.uint32).view(np.float32)
+    off = gait_offset(N)
+    rec[:, REC_HDR:REC_HDR + 12 * N] = traj
+    gbytes = rec[:, off:off + N].view(np.uint8)
+    gbytes[:, :] = gait
+    return rec
+
+
+def unpack_gait(rec: np.ndarray, horizon: int) -> np.ndarray:
+    off = gait_offset(horizon)
+    return np.ascontiguousarray(rec[:, off:off + horizon]).view(np.uint8).reshape(rec.shape[0], 4 * horizon)

@@ -1,0 +1,253 @@
+"""Host-side mirror of the reference's SolverMPC interface over the C ABI of libcmpc_hip.so.
+
+Two surfaces (see include/cmpc_solver.h):
+
+* the reference's single-instance functions, same names and argument meaning as
+  ``convexMPC_interface.h:44-52`` (``setup_problem``, ``update_solver_settings``,
+  ``update_x_drag``, ``update_problem_data_floats``, ``update_problem_data``,
+  ``get_solution``), so parity tests read like the reference's call protocol
+  (``ConvexMPCLocomotion.cpp:807-836``);
+* :class:`BatchSolver`, the reentrant batched API over device buffers (torch tensors on
+  ``cuda:*`` or raw pointers) — the hot path.
+
+There is no CPU fallback: if ``libcmpc_hip.so`` is missing or no GPU is present, calls fail.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .records import CmpcParams, make_params, record_words
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libcmpc_hip.so")
+
+# every symbol include/cmpc_solver.h declares (C linkage unless noted)
+EXPORTED_SYMBOLS = (
+    "setup_problem", "update_problem_data", "get_solution", "update_solver_settings",
+    "update_problem_data_floats", "_Z13update_x_dragf", "f_ext", "simulation_time",
+    "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
+    "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
+    "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing",
+)
+
+_lib = None
+_fp = ctypes.POINTER(ctypes.c_float)
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class CmpcError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libcmpc_hip.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise CmpcError(f"{path} not built: run __graft_entry__.build() "
+                        f"(or python quad-periodic-mpc_amd/build.py)")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    lib.setup_problem.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double]
+    lib.update_problem_data.argtypes = [_dp, _dp, _dp, _dp, _dp, ctypes.c_double, _dp, _dp,
+                                        ctypes.c_double, _ip]
+    lib.get_solution.argtypes = [ctypes.c_int]
+    lib.get_solution.restype = ctypes.c_double
+    lib.update_solver_settings.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                           ctypes.c_double, ctypes.c_double, ctypes.c_double]
+    lib.update_problem_data_floats.argtypes = [_fp, _fp, _fp, _fp, _fp, ctypes.c_float,
+                                               ctypes.c_float, ctypes.c_float, _fp, _fp,
+                                               ctypes.c_float, _ip]
+    lib._Z13update_x_dragf.argtypes = [ctypes.c_float]
+    lib.cmpc_record_words.argtypes = [ctypes.c_int]
+    lib.cmpc_batch_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(CmpcParams),
+                                      ctypes.c_int, ctypes.c_void_p]
+    lib.cmpc_batch_set_params.argtypes = [ctypes.c_void_p, ctypes.POINTER(CmpcParams)]
+    lib.cmpc_batch_destroy.argtypes = [ctypes.c_void_p]
+    lib.cmpc_batch_destroy.restype = None
+    lib.cmpc_batch_solve.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.cmpc_batch_solve_host.argtypes = [ctypes.c_void_p, _fp, ctypes.c_int, _fp, _u8p, _ip]
+    lib.cmpc_batch_condense.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+    lib.cmpc_batch_stream.argtypes = [ctypes.c_void_p]
+    lib.cmpc_batch_stream.restype = ctypes.c_void_p
+    lib.cmpc_last_error.restype = ctypes.c_char_p
+    lib.cmpc_batch_enable_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.cmpc_batch_read_timing.argtypes = [ctypes.c_void_p, _fp, _ip, _ip]
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load_library().cmpc_last_error().decode(errors="replace")
+        raise CmpcError(f"{what} failed ({rc}): {msg}")
+
+
+# ---------------------------------------------------------------------------------------------
+# Reference single-instance interface (convexMPC_interface.h:44-52)
+# ---------------------------------------------------------------------------------------------
+def _f32(a, n=None):
+    a = np.ascontiguousarray(a, np.float32)
+    if n is not None and a.size < n:
+        raise ValueError(f"expected >= {n} floats, got {a.size}")
+    return a
+
+
+def setup_problem(dt: float, horizon: int, mu: float, f_max: float) -> None:
+    load_library().setup_problem(dt, horizon, mu, f_max)
+
+
+def update_solver_settings(max_iter, rho, sigma, solver_alpha, terminate, use_jcqp) -> None:
+    load_library().update_solver_settings(int(max_iter), rho, sigma, solver_alpha, terminate, use_jcqp)
+
+
+def update_x_drag(x_drag: float) -> None:
+    load_library()._Z13update_x_dragf(float(x_drag))
+
+
+def update_problem_data_floats(p, v, q, w, r, roll, pitch, yaw, weights, state_trajectory, alpha,
+                               gait) -> None:
+    arrs = [_f32(p, 3), _f32(v, 3), _f32(q, 4), _f32(w, 3), _f32(r, 12)]
+    wts = _f32(weights, 12)
+    traj = _f32(state_trajectory)
+    g = np.ascontiguousarray(gait, np.int32)
+    load_library().update_problem_data_floats(
+        *[a.ctypes.data_as(_fp) for a in arrs], float(roll), float(pitch), float(yaw),
+        wts.ctypes.data_as(_fp), traj.ctypes.data_as(_fp), float(alpha), g.ctypes.data_as(_ip))
+
+
+def update_problem_data(p, v, q, w, r, yaw, weights, state_trajectory, alpha, gait) -> None:
+    arrs = [np.ascontiguousarray(a, np.float64) for a in (p, v, q, w, r)]
+    wts = np.ascontiguousarray(weights, np.float64)
+    traj = np.ascontiguousarray(state_trajectory, np.float64)
+    g = np.ascontiguousarray(gait, np.int32)
+    load_library().update_problem_data(
+        *[a.ctypes.data_as(_dp) for a in arrs], float(yaw), wts.ctypes.data_as(_dp),
+        traj.ctypes.data_as(_dp), float(alpha), g.ctypes.data_as(_ip))
+
+
+def get_solution(index: int) -> float:
+    return load_library().get_solution(int(index))
+
+
+def set_f_ext(values) -> None:
+    """Write the caller-owned global ``f_ext`` (ConvexMPCLocomotion.cpp:610)."""
+    arr = (ctypes.c_float * 6).in_dll(load_library(), "f_ext")
+    for i, x in enumerate(values):
+        arr[i] = float(x)
+
+
+def set_simulation_time(t: float) -> None:
+    ctypes.c_float.in_dll(load_library(), "simulation_time").value = float(t)
+
+
+# ---------------------------------------------------------------------------------------------
+# Batched API
+# ---------------------------------------------------------------------------------------------
+def _ptr(t) -> int:
+    if t is None:
+        return 0
+    if hasattr(t, "data_ptr"):
+        if not t.is_cuda:
+            raise CmpcError("BatchSolver.solve expects device tensors")
+        return t.data_ptr()
+    return int(t)
+
+
+class BatchSolver:
+    """Reentrant batched solver bound to one HIP stream (``cmpc_batch_*``)."""
+
+    def __init__(self, params: CmpcParams | None = None, max_batch: int = 65536, stream=None,
+                 horizon: int = 10):
+        self.lib = load_library()
+        self.params = params if params is not None else make_params(horizon)
+        self.max_batch = int(max_batch)
+        h = ctypes.c_void_p()
+        s = None
+        if stream is not None:
+            s = ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+        _check(self.lib.cmpc_batch_create(ctypes.byref(h), ctypes.byref(self.params),
+                                          self.max_batch, s), "cmpc_batch_create")
+        self._h = h
+
+    @property
+    def horizon(self) -> int:
+        return self.params.horizon
+
+    @property
+    def record_words(self) -> int:
+        return record_words(self.params.horizon)
+
+    @property
+    def stream_handle(self) -> int:
+        return self.lib.cmpc_batch_stream(self._h)
+
+    def set_params(self, params: CmpcParams) -> None:
+        _check(self.lib.cmpc_batch_set_params(self._h, ctypes.byref(params)), "set_params")
+        self.params = params
+
+    def solve(self, records, forces, status, iters=None, batch: int | None = None) -> None:
+        """Asynchronous device solve on the handle's stream (torch tensors or raw pointers)."""
+        if batch is None:
+            batch = records.shape[0]
+        if batch > self.max_batch:
+            raise CmpcError(f"batch {batch} > max_batch {self.max_batch}")
+        if hasattr(records, "shape"):
+            assert records.shape[-1] == self.record_words, "record stride mismatch"
+            assert forces.numel() >= batch * 12 * self.horizon and status.numel() >= batch
+        _check(self.lib.cmpc_batch_solve(self._h, _ptr(records), int(batch), _ptr(forces),
+                                         _ptr(status), _ptr(iters)), "cmpc_batch_solve")
+
+    def solve_host(self, records: np.ndarray):
+        """Host arrays in/out (H2D + solve + D2H, synchronous) -> (forces, status, iters)."""
+        records = np.ascontiguousarray(records, np.float32)
+        B = records.shape[0]
+        assert records.shape[1] == self.record_words
+        forces = np.zeros((B, 12 * self.horizon), np.float32)
+        status = np.zeros(B, np.uint8)
+        iters = np.zeros(B, np.int32)
+        _check(self.lib.cmpc_batch_solve_host(self._h, records.ctypes.data_as(_fp), B,
+                                              forces.ctypes.data_as(_fp),
+                                              status.ctypes.data_as(_u8p),
+                                              iters.ctypes.data_as(_ip)), "cmpc_batch_solve_host")
+        return forces, status, iters
+
+    def condense(self, records, H, g, batch: int | None = None) -> None:
+        """Full (no elimination) qH [B,12N,12N] / qg [B,12N] on device — parity hook."""
+        if batch is None:
+            batch = records.shape[0]
+        _check(self.lib.cmpc_batch_condense(self._h, _ptr(records), int(batch), _ptr(H), _ptr(g)),
+               "cmpc_batch_condense")
+
+    def enable_timing(self, steps: int) -> None:
+        """Record HIP events around each size-class launch of the next ``steps`` solves."""
+        self._timing_steps = int(steps)
+        _check(self.lib.cmpc_batch_enable_timing(self._h, int(steps)), "enable_timing")
+
+    def read_timing(self):
+        """-> (ms [steps, 2] per class launch, class-1 overflow count of the last solve)."""
+        n = getattr(self, "_timing_steps", 0)
+        ms = np.zeros(2 * max(n, 1), np.float32)
+        rec = ctypes.c_int(0)
+        ovf = ctypes.c_int(0)
+        _check(self.lib.cmpc_batch_read_timing(self._h, ms.ctypes.data_as(_fp), ctypes.byref(rec),
+                                               ctypes.byref(ovf)), "read_timing")
+        return ms[:2 * rec.value].reshape(rec.value, 2), ovf.value
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.cmpc_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

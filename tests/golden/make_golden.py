@@ -1,0 +1,71 @@
+"""Generate the committed golden fixtures (tests/golden/*.npz) with the oracle.
+
+Outputs of the reference pipeline run here: the fp32 condensation restatement
+(oracle/cmpc_oracle.c, SolverMPC.cpp:566-950) chained with the reference's own vendored
+qpOASES 3.2.0 compiled from /root/reference (oracle/_ref, SolverMPC.cpp:952-982).
+Run from the repo root:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+cm = importlib.import_module("quad-periodic-mpc_amd")
+from oracle import oracle as orc  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def edge_records(N: int) -> np.ndarray:
+    """All-swing, one stance foot, all-stance, x_drag extremes, upside-down-ish orientation."""
+    base = cm.make_instances(6, N, seed=99, random_contact_frac=0.0)
+    gait = cm.unpack_gait(base, N).astype(np.int32)
+    gait[0, :] = 0                       # all swing: n = 0
+    gait[1, :] = 0
+    gait[1, 0::4] = 1                    # one foot in stance every step
+    gait[2, :] = 1                       # all stance: n = 12 N
+    gait[3, :] = 0
+    gait[3, :4] = 1                      # stance only at the first step
+    recs = base.copy()
+    off = cm.records.gait_offset(N)
+    recs[:, off:off + N] = np.ascontiguousarray(gait.astype(np.uint8)).view(np.float32).reshape(6, N)
+    recs[4, cm.records.REC_XDRAG] = 0.5
+    recs[5, cm.records.REC_XDRAG] = -0.5
+    return recs
+
+
+def build_set(name, records, prm, cond_count=0):
+    q, st, nw = orc.ref_solve_batch(records, prm, nthreads=8)
+    out = dict(records=records, horizon=prm.horizon, dt=prm.dt, mu=prm.mu, f_max=prm.f_max,
+               weights=np.array(prm.weights, np.float32), alpha=prm.alpha, q_ref=q, status=st,
+               nwsr=nw)
+    if cond_count:
+        qH, qg, Adt, Bdt, Qdt, x0 = [], [], [], [], [], []
+        for i in range(cond_count):
+            c = orc.condense(records[i], prm)
+            qH.append(c["qH"]); qg.append(c["qg"]); Adt.append(c["Adt"]); Bdt.append(c["Bdt"])
+            Qdt.append(c["Qdt"]); x0.append(c["x0"])
+        out.update(qH=np.stack(qH), qg=np.stack(qg), Adt=np.stack(Adt), Bdt=np.stack(Bdt),
+                   Qdt=np.stack(Qdt), x0=np.stack(x0))
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
+    print(name, records.shape, "status", np.bincount(st), "nWSR mean", nw.mean())
+
+
+def main():
+    orc.build()
+    build_set("n10_mixed", cm.make_instances(48, 10, seed=1001), cm.make_params(10), cond_count=4)
+    build_set("n10_stress", cm.make_instances(16, 10, seed=1002, stress=True), cm.make_params(10))
+    build_set("n10_edge", edge_records(10), cm.make_params(10), cond_count=1)
+    build_set("n16_trot", cm.make_instances(8, 16, seed=1003, random_contact_frac=0.0), cm.make_params(16))
+    build_set("n19_mixed", cm.make_instances(8, 19, seed=1004), cm.make_params(19))
+    build_set("n20_trot", cm.make_instances(8, 20, seed=1005, random_contact_frac=0.0),
+              cm.make_params(20), cond_count=1)
+
+
+if __name__ == "__main__":
+    main()
