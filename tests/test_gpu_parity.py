@@ -71,8 +71,9 @@ def test_edge_cases(cm, solver_mod):
     prm = golden_params(cm, g)
     f, st, it = gpu_solve(solver_mod, prm, g["records"])
     assert np.all(f[0] == 0.0) and st[0] == 0          # all swing -> zero forces
-    gait = cm.unpack_gait(g["records"], 10)
-    assert np.all(f[gait == 0] == 0.0)                 # swing legs exactly zero (SolverMPC.cpp:975)
+    gait = cm.unpack_gait(g["records"], 10)            # [B, 4N] per foot step
+    swing = np.repeat(gait == 0, 3, axis=1)            # [B, 12N] per force component
+    assert np.all(f[swing] == 0.0)                     # swing legs exactly zero (SolverMPC.cpp:975)
 
 
 @pytest.mark.parametrize("N,stress,frac", [(10, False, 0.25), (10, True, 0.25), (10, False, 1.0),
