@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "cmpc_kernels.h"
 
 namespace cmpc {
@@ -69,11 +71,10 @@ __device__ __forceinline__ void bsync() {
   __syncthreads();
 }
 
-template <int W>
-struct Shared {
-  static constexpr int NV = 64 * W;
-  static constexpr int LDM = NV + 4;      // row stride of M (16-B aligned rows)
-  float M[NV * LDM];                      // raw Cholesky rows, then R (row-major, q x q)
+// LDS common to every size class (small: ~8 KB for NV = 64).
+template <int NV_>
+struct SharedCommon {
+  static constexpr int NV = NV_;
   float BdtT[12][16];                     // Bdt columns (13 used)
   float traj[MAXN * 12];
   float E[MAXN][16];                      // state error e_i = x_{i+1}(U=0) - X_d,i
@@ -82,12 +83,7 @@ struct Shared {
   float bufB[NV + 4];
   float dfull[NV + 4];                    // d = J' n+
   float dmask[NV + 4];                    // d with entries < q zeroed
-  float tsv[NV + 4];                      // suffix norms
-  float cs[2 * NV + 8];                   // Givens (c, s) pairs
   float xs[NV + 4];                       // current primal iterate
-  float rvec[NV + 4];                     // dual step r
-  float u[NV + 4];                        // duals of the active set
-  int act[NV + 4];                        // active constraint ids (6 * foot + type)
   float red_f[8];
   int red_i[8];
   float sub[4 * MAXN];                    // ub of each stance foot step (gait * f_max)
@@ -100,8 +96,24 @@ struct Shared {
   int ctrl[4];
 };
 
+// The 64-lane class keeps U, J and the QP's R implicitly in registers: only the common part.
+struct SharedW1 : SharedCommon<64> {};
+
+// Wider classes keep the raw Cholesky rows / the QP's R explicitly in LDS (region M).
 template <int W>
-__device__ __forceinline__ float block_sum(float v, Shared<W>& sh) {
+struct Shared : SharedCommon<64 * W> {
+  static constexpr int NVW = 64 * W;
+  static constexpr int LDM = NVW + 4;     // row stride of M (16-B aligned rows)
+  float M[NVW * LDM];                     // raw Cholesky rows, then R (row-major, q x q)
+  float tsv[NVW + 4];                     // suffix norms
+  float cs[2 * NVW + 8];                  // Givens (c, s) pairs
+  float rvec[NVW + 4];                    // dual step r
+  float u[NVW + 4];                       // duals of the active set
+  int act[NVW + 4];                       // active constraint ids (6 * foot + type)
+};
+
+template <int W, class SH>
+__device__ __forceinline__ float block_sum(float v, SH& sh) {
   v = wave_sum(v);
   if constexpr (W == 1) {
     return v;
@@ -117,8 +129,8 @@ __device__ __forceinline__ float block_sum(float v, Shared<W>& sh) {
   }
 }
 
-template <int W>
-__device__ __forceinline__ float block_max(float v, Shared<W>& sh) {
+template <int W, class SH>
+__device__ __forceinline__ float block_max(float v, SH& sh) {
   v = wave_max(v);
   if constexpr (W == 1) {
     return v;
@@ -134,8 +146,8 @@ __device__ __forceinline__ float block_max(float v, Shared<W>& sh) {
   }
 }
 
-template <int W>
-__device__ __forceinline__ void block_argmin(float& v, int& idx, Shared<W>& sh) {
+template <int W, class SH>
+__device__ __forceinline__ void block_argmin(float& v, int& idx, SH& sh) {
   wave_argmin(v, idx);
   if constexpr (W > 1) {
     const int wv = threadIdx.x >> 6;
@@ -153,8 +165,8 @@ __device__ __forceinline__ void block_argmin(float& v, int& idx, Shared<W>& sh) 
   }
 }
 
-template <int W>
-__device__ __forceinline__ float block_suffix_sum(float v, Shared<W>& sh) {
+template <int W, class SH>
+__device__ __forceinline__ float block_suffix_sum(float v, SH& sh) {
   const int lane = threadIdx.x & 63;
   v = wave_suffix_sum(v, lane);
   if constexpr (W > 1) {
@@ -169,6 +181,34 @@ __device__ __forceinline__ float block_suffix_sum(float v, Shared<W>& sh) {
   }
   return v;
 }
+
+template <int I, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < E) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, E>(f);
+  }
+}
+
+__device__ __forceinline__ float rl(float x, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
+}
+__device__ __forceinline__ int rli(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
+// An SGPR value the compiler cannot see through: keeps per-iteration readlanes of an unrolled
+// loop inside their iteration (otherwise all of them are hoisted, ~128 SGPRs live -> spills).
+__device__ __forceinline__ int opaque(int x) {
+  x = __builtin_amdgcn_readfirstlane(x);
+  asm volatile("" : "+s"(x));
+  return x;
+}
+// Per-step lane predicates built on opaque() so LICM cannot hoist 64 compare masks (128 SGPRs)
+// out of the surrounding loops.
+__device__ __forceinline__ bool lane_eq(int k) { return (int)threadIdx.x == opaque(k); }
+__device__ __forceinline__ bool lane_gt(int k) { return (int)threadIdx.x > opaque(k); }
+__device__ __forceinline__ bool lane_lt(int k) { return (int)threadIdx.x < opaque(k); }
+// lane `k` gets `val`, other lanes keep `x`
+__device__ __forceinline__ float wl(float val, int k, float x) { return lane_eq(k) ? val : x; }
+__device__ __forceinline__ int wli(int val, int k, int x) { return lane_eq(k) ? val : x; }
 
 // ---------------------------------------------------------------------------------------------
 // Discretised model pieces (SolverMPC.cpp:260-279 + 96-107 in closed form; A_c^3 = 0 so
@@ -223,20 +263,19 @@ __device__ __forceinline__ float dot13(const float* a, const float* b) {
 // ---------------------------------------------------------------------------------------------
 // The fused per-instance solve.
 // ---------------------------------------------------------------------------------------------
-template <int W>
-__device__ void solve_instance(const float* __restrict__ rec, const KParams& P, Shared<W>& sh,
-                               float* __restrict__ fout, uint8_t* __restrict__ st_out,
-                               int32_t* __restrict__ it_out, int* __restrict__ ovf_list,
-                               int* __restrict__ ovf_count, int inst, float* __restrict__ Hout,
-                               float* __restrict__ gout) {
+// Stages shared by every size class: stance table + elimination (SolverMPC.cpp:859-894), robot
+// state + discretised model (RobotState.cpp:9-50, SolverMPC.cpp:260-279, 96-107), and the
+// condensation of thread v's row of the reduced Hessian [H | g] into slot[0..NV].
+// Returns the reduced size n (> NV: the instance needs a wider class; slot untouched).
+template <int W, class SH>
+__device__ __forceinline__ int prepare_instance(const float* __restrict__ rec, const KParams& P, SH& sh,
+                                                bool condense_only, float (&slot)[64 * W + 1],
+                                                int& nfs_out) {
   constexpr int NV = 64 * W;
   constexpr int NT = 64 * W;
-  constexpr int LDM = Shared<W>::LDM;
-  const int v = threadIdx.x;           // reduced variable / row owned by this thread
+  const int v = threadIdx.x;
   const int lane = v & 63;
   const int N = P.N;
-  const bool condense_only = (Hout != nullptr);
-
   // ---- stance table: ub = gait * f_max, eliminated iff near_zero(ub) (SolverMPC.cpp:869-894)
   const unsigned char* gait = reinterpret_cast<const unsigned char*>(rec + CMPC_REC_HDR + 12 * N);
   for (int t = v; t < 4 * N; t += NT) {
@@ -264,19 +303,8 @@ __device__ void solve_instance(const float* __restrict__ rec, const KParams& P, 
   bsync<W>();
   const int nfs = sh.ctrl[0];
   const int n = 3 * nfs;
-  if (n > NV && condense_only) return;
-  if (n > NV && ovf_list == nullptr) {  // no wider class available
-    for (int t = v; t < 12 * N; t += NT) fout[t] = 0.f;
-    if (v == 0) { st_out[0] = CMPC_BAD_INPUT; if (it_out) it_out[0] = 0; }
-    return;
-  }
-  if (n > NV) {  // needs a wider workgroup: hand the instance to the next size class
-    if (v == 0) {
-      const int slot = atomicAdd(ovf_count, 1);
-      ovf_list[slot] = inst;
-    }
-    return;
-  }
+  nfs_out = nfs;
+  if (n > NV) return n;  // the caller hands the instance to a wider class
   for (int t = v; t < NV; t += NT) {
     if (t < n) {
       const int fs = sh.sfs[t / 3];
@@ -440,7 +468,6 @@ __device__ void solve_instance(const float* __restrict__ rec, const KParams& P, 
   bsync<W>();
 
   // ---- condensation: thread v fills its row of the (reduced) Hessian + gradient ------------
-  float slot[NV + 1];
 #pragma unroll
   for (int c = 0; c <= NV; c++) slot[c] = (c == v && v >= n) ? 1.f : 0.f;  // identity padding
   {
@@ -480,17 +507,48 @@ __device__ void solve_instance(const float* __restrict__ rec, const KParams& P, 
 #pragma unroll
       for (int w = 0; w < NV; w++) {
         if (w >= base && w < end) {
-          const int cw = sh.varcol[w];
+          const int cw = sh.varcol[opaque(w)];  // opaque: keep this load inside its block step
           float bw[13];
 #pragma unroll
           for (int j = 0; j < 13; j++) bw[j] = sh.BdtT[cw][j];
-          float val = 2.f * dot13(bw, z);
-          if (w == v) val += P.alpha2;
+          const float val = 2.f * dot13(bw, z);
           slot[w] = real ? val : slot[w];
         }
       }
     }
     slot[NV] = real ? gv : 0.f;
+    // + 2 alpha on the diagonal (qH = 2 (B'SB + alpha I), SolverMPC.cpp:806)
+#pragma unroll
+    for (int c = 0; c < NV; c++) slot[c] += (c == v && real) ? P.alpha2 : 0.f;
+  }
+
+  return n;
+}
+
+template <int W>
+__device__ __forceinline__ void solve_instance(const float* __restrict__ rec, const KParams& P, Shared<W>& sh,
+                               float* __restrict__ fout, uint8_t* __restrict__ st_out,
+                               int32_t* __restrict__ it_out, int* __restrict__ ovf_list,
+                               int* __restrict__ ovf_count, int inst, float* __restrict__ Hout,
+                               float* __restrict__ gout) {
+  constexpr int NV = 64 * W;
+  constexpr int NT = 64 * W;
+  constexpr int LDM = Shared<W>::LDM;
+  const int v = threadIdx.x;           // reduced variable / row owned by this thread
+  const int N = P.N;
+  const bool condense_only = (Hout != nullptr);
+  float slot[NV + 1];
+  int nfs = 0;
+  const int n = prepare_instance<W>(rec, P, sh, condense_only, slot, nfs);
+  if (n > NV) {
+    if (condense_only) return;
+    if (ovf_list != nullptr) {  // hand the instance to the next size class
+      if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
+      return;
+    }
+    for (int t = v; t < 12 * N; t += NT) fout[t] = 0.f;  // no wider class available
+    if (v == 0) { st_out[0] = CMPC_BAD_INPUT; if (it_out) it_out[0] = 0; }
+    return;
   }
 
   if (condense_only) {  // parity hook: write the (full, nothing eliminated) qH row and qg
@@ -800,6 +858,348 @@ __device__ void solve_instance(const float* __restrict__ rec, const KParams& P, 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// 64-lane class, register-resident. One wavefront per instance; lane v owns row v of H -> U ->
+// J = U^{-1} in slot[0..63] (+ slot[64] = g -> y). Every loop over matrix columns is unrolled
+// at compile time (static_for) so register indices are constants; LDS only broadcasts one row
+// per step. The QP's R factor is never stored: R[i][j] = J[:,i]' n_j is recomputed from J
+// (registers) and the 2-sparse friction-pyramid normals n_j ("implicit R").
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wsync() {
+  // single-wavefront workgroup: orders LDS traffic between lanes without an s_barrier
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+struct Cons {
+  int ia, iz;
+  float ca, cb, bp;
+};
+// constraint id c = 6 s + t of stance foot step s (reduced vars 3s, 3s+1, 3s+2):
+//   t = 0..3: +-fx/mu + fz >= 0, +-fy/mu + fz >= 0 ; t = 4: fz >= 0 ; t = 5: -fz >= -ub
+// (fmat rows of SolverMPC.cpp:657-665 with lb = 0, ub = BIG / gait*f_max)
+__device__ __forceinline__ Cons decode_cons(int c, float mui, const float* sub) {
+  Cons k;
+  const int sft = c / 6, t = c - 6 * (c / 6);
+  k.iz = 3 * sft + 2;
+  if (t < 4) {
+    k.ia = 3 * sft + (t >> 1);
+    k.ca = (t & 1) ? -mui : mui;
+    k.cb = 1.f;
+    k.bp = 0.f;
+  } else {
+    k.ia = k.iz;
+    k.ca = 0.f;
+    k.cb = (t == 4) ? 1.f : -1.f;
+    k.bp = (t == 4) ? 0.f : -sub[sft];
+  }
+  return k;
+}
+
+// Bordered Cholesky [H | g] = U'[U | y] (lane v: row v). Returns y_v; slot <- U row v with
+// zeros below the diagonal.
+__device__ __forceinline__ float chol_w1(float (&slot)[65], int n, SharedW1& sh, int& status) {
+  constexpr int NV = 64;
+  const int v = threadIdx.x;
+  // ---- bordered Cholesky [H | g] = U'[U | y], right-looking, pivot row k broadcast via LDS --
+  float my_inv = 1.f;
+  static_for<0, NV>([&](auto KC) {
+    constexpr int k = decltype(KC)::value;
+    constexpr int c0 = k & ~3;
+    if (k < n) {
+      float d2 = rl(slot[k], k);
+      if (!(d2 > 0.f)) { status = CMPC_NOT_PD; d2 = 1e-30f; }
+      const float inv = rsqrtf(d2);
+      my_inv = wl(inv, k, my_inv);
+      float* buf = sh.bufA[k & 1];
+      if (lane_eq(k)) {
+#pragma unroll
+        for (int c = c0; c < NV; c += 4)
+          *reinterpret_cast<float4*>(&buf[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
+        buf[NV] = slot[NV];
+      }
+      wsync();
+      const float a = lane_gt(k) ? -buf[v] * inv * inv : 0.f;
+#pragma unroll
+      for (int c = c0; c < NV; c += 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(&buf[c]);
+        slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
+        slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
+        slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
+        slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+      }
+      slot[NV] = fmaf(a, buf[NV], slot[NV]);
+    }
+  });
+  // scale row v by 1/U[v][v] (raw diagonal d^2 -> d), y_v = raw g row / U[v][v]; zero c < v
+  const float yv = slot[NV] * my_inv;
+#pragma unroll
+  for (int c = 0; c < NV; c++) slot[c] = (c < v) ? 0.f : slot[c] * my_inv;
+
+  return yv;
+}
+
+// J = U^{-1} in place (lane v: row v of J).
+__device__ __forceinline__ void inv_w1(float (&slot)[65], int n, SharedW1& sh) {
+  constexpr int NV = 64;
+  const int v = threadIdx.x;
+  // ---- J = U^{-1} in place, rows l descending (in-place scheme: DESIGN.md) ------------------
+  static_for<0, NV>([&](auto IC) {
+    constexpr int l = NV - 1 - decltype(IC)::value;
+    constexpr int c0 = l & ~3;
+    if (l < n) {
+      const float inv_l = 1.f / rl(slot[l], l);
+      float* buf = sh.bufA[l & 1];
+      if (lane_eq(l)) {
+#pragma unroll
+        for (int c = c0; c < NV; c += 4) {
+          float w4[4];
+#pragma unroll
+          for (int t = 0; t < 4; t++) {
+            const int cc = c + t;
+            w4[t] = (cc < l) ? 0.f : ((cc == l) ? inv_l - 1.f : -slot[cc] * inv_l);
+          }
+          *reinterpret_cast<float4*>(&buf[c]) = make_float4(w4[0], w4[1], w4[2], w4[3]);
+        }
+      }
+      wsync();
+      const float u = lane_lt(l) ? slot[l] : 0.f;
+#pragma unroll
+      for (int c = c0; c < NV; c += 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(&buf[c]);
+        slot[c + 0] = fmaf(u, r4.x, slot[c + 0]);
+        slot[c + 1] = fmaf(u, r4.y, slot[c + 1]);
+        slot[c + 2] = fmaf(u, r4.z, slot[c + 2]);
+        slot[c + 3] = fmaf(u, r4.w, slot[c + 3]);
+      }
+      // lane l finalises its row (branch-free: a divergent branch here would force the register
+      // allocator to keep two copies of the row live)
+      const float fl = wl(-inv_l, l, 1.f);
+#pragma unroll
+      for (int c = l + 1; c < NV; c++) slot[c] *= fl;
+      slot[l] = wl(inv_l, l, slot[l]);
+    }
+  });
+
+}
+
+// Unconstrained minimiser x = -J y (lane v: x_v).
+__device__ __forceinline__ float xsol_w1(const float (&slot)[65], int n, float yv, SharedW1& sh) {
+  constexpr int NV = 64;
+  const int v = threadIdx.x;
+  // ---- unconstrained minimiser x = -J y -----------------------------------------------------
+  sh.dfull[v] = yv;
+  wsync();
+  float xv = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; c += 4) {
+    const float4 y4 = *reinterpret_cast<const float4*>(&sh.dfull[c]);
+    xv = fmaf(slot[c + 0], y4.x, xv);
+    xv = fmaf(slot[c + 1], y4.y, xv);
+    xv = fmaf(slot[c + 2], y4.z, xv);
+    xv = fmaf(slot[c + 3], y4.w, xv);
+  }
+  xv = (v < n) ? -xv : 0.f;
+  wsync();
+
+  return xv;
+}
+
+// Goldfarb-Idnani on the friction pyramids; J in slot (updated), x in xv. Returns iterations.
+__device__ __forceinline__ int gi_w1(float (&slot)[65], float& xv, int n, int nfs, const KParams& P,
+                                     SharedW1& sh, int& status) {
+  constexpr int NV = 64;
+  const int v = threadIdx.x;
+  // ---- Goldfarb-Idnani dual active set, R implicit ----------------------------------------
+  const float mui = P.mu_inv;
+  const float fnorm = 1.f / sqrtf(mui * mui + 1.f);
+  int q = 0;            // active-set size (uniform)
+  int act_v = 0;        // lane j < q: id of the j-th active constraint
+  float u_v = 0.f;      // lane j < q: its dual
+  int iters = 0;
+  const int cap = P.max_iter;
+  if (status == CMPC_OK) {
+    for (;;) {
+      sh.xs[v] = xv;
+      wsync();
+      float best = 0.f;
+      int bid = 0x7fffffff;
+      if (v < nfs) {
+        const int s = v;
+        const float fx = sh.xs[3 * s], fy = sh.xs[3 * s + 1], fz = sh.xs[3 * s + 2];
+        float sl[6];
+        sl[0] = (mui * fx + fz) * fnorm;
+        sl[1] = (-mui * fx + fz) * fnorm;
+        sl[2] = (mui * fy + fz) * fnorm;
+        sl[3] = (-mui * fy + fz) * fnorm;
+        sl[4] = fz;
+        sl[5] = sh.sub[s] - fz;
+#pragma unroll
+        for (int t = 0; t < 6; t++)
+          if (!sh.cflag[6 * s + t] && sl[t] < best) { best = sl[t]; bid = 6 * s + t; }
+      }
+      const float xmax = wave_max(fabsf(xv));
+      wave_argmin(best, bid);
+      const float tol = 1e-5f * fmaxf(1.f, xmax);
+      if (bid == 0x7fffffff || best >= -tol) break;
+
+      const int p = __builtin_amdgcn_readfirstlane(bid);
+      const Cons cp = decode_cons(p, mui, sh.sub);
+      float up = 0.f;
+      for (;;) {
+        if (++iters > cap) { status = CMPC_MAX_ITER; break; }
+        // d = J' n+  (rows ia, iz of J through LDS)
+        if (v == cp.ia) {
+#pragma unroll
+          for (int c = 0; c < NV; c += 4)
+            *reinterpret_cast<float4*>(&sh.bufA[0][c]) =
+                make_float4(cp.ca * slot[c], cp.ca * slot[c + 1], cp.ca * slot[c + 2], cp.ca * slot[c + 3]);
+        }
+        if (v == cp.iz) {
+#pragma unroll
+          for (int c = 0; c < NV; c += 4)
+            *reinterpret_cast<float4*>(&sh.bufB[c]) =
+                make_float4(cp.cb * slot[c], cp.cb * slot[c + 1], cp.cb * slot[c + 2], cp.cb * slot[c + 3]);
+        }
+        wsync();
+        const float dv = sh.bufA[0][v] + sh.bufB[v];
+        sh.dfull[v] = dv;
+        sh.dmask[v] = (v >= q) ? dv : 0.f;
+        wsync();
+        // z = J2 d2, zn = |d2|^2 (= z' n+), dn = |d|^2
+        float zv = 0.f, zn = 0.f, dn = 0.f;
+#pragma unroll
+        for (int c = 0; c < NV; c += 4) {
+          const float4 m4 = *reinterpret_cast<const float4*>(&sh.dmask[c]);
+          const float4 f4 = *reinterpret_cast<const float4*>(&sh.dfull[c]);
+          zv = fmaf(slot[c + 0], m4.x, zv);
+          zv = fmaf(slot[c + 1], m4.y, zv);
+          zv = fmaf(slot[c + 2], m4.z, zv);
+          zv = fmaf(slot[c + 3], m4.w, zv);
+          zn += m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
+          dn += f4.x * f4.x + f4.y * f4.y + f4.z * f4.z + f4.w * f4.w;
+        }
+        // r = R^{-1} d1 with R[i][j] = J[:,i]' n_j: back substitution through the vector
+        // m = sum_{j>i} r_j n_j, so sum_{j>i} R[i][j] r_j = J[:,i]' m (one column dot per i)
+        float m = 0.f, rv = 0.f;
+        static_for<0, NV>([&](auto IC) {
+          constexpr int i = NV - 1 - decltype(IC)::value;
+          if (i < q) {
+            const Cons ci = decode_cons(rli(act_v, opaque(i)), mui, sh.sub);
+            const float Rii = ci.ca * rl(slot[i], ci.ia) + ci.cb * rl(slot[i], ci.iz);
+            const float sdot = wave_sum(slot[i] * m);
+            const float ri = (rl(dv, i) - sdot) / Rii;
+            rv = wl(ri, i, rv);
+            m = wl(fmaf(ci.ca, ri, rl(m, ci.ia)), ci.ia, m);
+            m = wl(fmaf(ci.cb, ri, rl(m, ci.iz)), ci.iz, m);
+          }
+        });
+        // partial (dual) step t1 and full (primal) step t2
+        float t1 = kBigF;
+        int kk = 0x7fffffff;
+        if (v < q && rv > 0.f) { t1 = fmaxf(u_v / rv, 0.f); kk = v; }
+        wave_argmin(t1, kk);
+        const float spv = fmaf(cp.ca, rl(xv, cp.ia), fmaf(cp.cb, rl(xv, cp.iz), -cp.bp));
+        const bool zero_step = !(zn > 1e-9f * dn);
+        const float t2 = zero_step ? kBigF : -spv / zn;
+        const float t = fminf(t1, t2);
+        if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
+        if (v < q) u_v = fmaf(-t, rv, u_v);
+        up += t;
+        if (!zero_step) xv = fmaf(t, zv, xv);
+        if (!zero_step && t2 <= t1) {
+          // ---- add p: Givens zeroing d[q+1..n-1] into d[q]; params from suffix norms ----
+          const float dsq = (v >= q && v < n) ? dv * dv : 0.f;
+          const float ts = sqrtf(wave_suffix_sum(dsq, v));
+          const float ts_prev = __shfl_up(ts, 1, 64);
+          const float d_prev = __shfl_up(dv, 1, 64);
+          float cj = 1.f, sj = 0.f;
+          if (v > q && v < n && ts_prev > 0.f) {
+            cj = d_prev / ts_prev;
+            sj = ((v == n - 1) ? dv : ts) / ts_prev;
+          }
+          static_for<0, NV - 1>([&](auto IC) {
+            constexpr int j = NV - 1 - decltype(IC)::value;  // 63 .. 1
+            if ((unsigned)(j - q - 1) < (unsigned)(n - q - 1)) {  // q < j < n, not hoistable
+              const int jj = opaque(j);
+              const float c = rl(cj, jj), sn = rl(sj, jj);
+              const float a0 = slot[j - 1], b0 = slot[j];
+              slot[j - 1] = fmaf(c, a0, sn * b0);
+              slot[j] = fmaf(-sn, a0, c * b0);
+            }
+          });
+          act_v = wli(p, q, act_v);
+          u_v = wl(up, q, u_v);
+          if (v == 0) sh.cflag[p] = 1;
+          q++;
+          break;
+        }
+        // ---- drop active constraint kk, then re-triangularise (implicit R) ----------------
+        {
+          const int k = __builtin_amdgcn_readfirstlane(kk);
+          const int dropped = rli(act_v, k);
+          if (v == 0) sh.cflag[dropped] = 0;
+          const int a_nx = __shfl_down(act_v, 1, 64);
+          const float u_nx = __shfl_down(u_v, 1, 64);
+          if (v >= k && v < q - 1) { act_v = a_nx; u_v = u_nx; }
+          static_for<0, NV - 1>([&](auto JC) {
+            constexpr int j = decltype(JC)::value;  // 0 .. 62
+            if (j >= k && j < q - 1) {
+              const Cons cj2 = decode_cons(rli(act_v, opaque(j)), mui, sh.sub);
+              const float a0 = cj2.ca * rl(slot[j], cj2.ia) + cj2.cb * rl(slot[j], cj2.iz);
+              const float b0 = cj2.ca * rl(slot[j + 1], cj2.ia) + cj2.cb * rl(slot[j + 1], cj2.iz);
+              const float h = sqrtf(a0 * a0 + b0 * b0);
+              float c = 1.f, sn = 0.f;
+              if (h > 0.f) { c = a0 / h; sn = b0 / h; }
+              const float x0 = slot[j], x1 = slot[j + 1];
+              slot[j] = fmaf(c, x0, sn * x1);
+              slot[j + 1] = fmaf(-sn, x0, c * x1);
+            }
+          });
+          q--;
+        }
+      }
+      if (status != CMPC_OK) break;
+    }
+  }
+
+  return iters;
+}
+
+__device__ __forceinline__ void solve_w1(const float* __restrict__ rec, const KParams& P, SharedW1& sh,
+                         float* __restrict__ fout, uint8_t* __restrict__ st_out,
+                         int32_t* __restrict__ it_out, int* __restrict__ ovf_list,
+                         int* __restrict__ ovf_count, int inst) {
+  constexpr int NV = 64;
+  const int v = threadIdx.x;
+  const int N = P.N;
+  float slot[NV + 1];
+  int nfs = 0;
+  const int n = prepare_instance<1>(rec, P, sh, false, slot, nfs);
+  if (n > NV) {
+    if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
+    return;
+  }
+
+  int status = CMPC_OK;
+  const float yv = chol_w1(slot, n, sh, status);
+  inv_w1(slot, n, sh);
+  float xv = xsol_w1(slot, n, yv, sh);
+  const int iters = gi_w1(slot, xv, n, nfs, P, sh, status);
+
+  // ---- scatter forces (q_soln layout: 12 k + 3 leg + axis; swing -> 0) --------------------
+  const bool ok = (status == CMPC_OK);
+  if (v < n) fout[12 * sh.varblk[v] + sh.varcol[v]] = ok ? xv : 0.f;
+  for (int t = v; t < 12 * N; t += NV)
+    if (!sh.stance[t / 3] || !ok) fout[t] = 0.f;
+  if (v == 0) {
+    st_out[0] = (uint8_t)status;
+    if (it_out) it_out[0] = iters;
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
@@ -820,6 +1220,17 @@ __global__ __launch_bounds__(64 * W) void cmpc_solve_kernel(
                       nullptr, nullptr);
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(64) void cmpc_solve_w1_kernel(
+    const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
+    uint8_t* __restrict__ status, int32_t* __restrict__ iters, int* __restrict__ ovf_list,
+    int* __restrict__ ovf_count) {
+  __shared__ SharedW1 sh;
+  const int inst = blockIdx.x;
+  if (inst >= batch) return;
+  solve_w1(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N, status + inst,
+           iters ? iters + inst : nullptr, ovf_list, ovf_count, inst);
 }
 
 template <int W>
@@ -848,8 +1259,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   if (ev) (void)hipEventRecord(ev[0], stream);
   // class 1: one 64-thread workgroup per instance; instances with > 64 stance variables are
   // appended to list1
-  hipLaunchKernelGGL(cmpc_solve_kernel<1>, dim3(batch), dim3(64), 0, stream, d_recs, batch, P,
-                     d_forces, d_status, d_iters, nullptr, nullptr, list1, cnt1);
+  hipLaunchKernelGGL(cmpc_solve_w1_kernel, dim3(batch), dim3(64), 0, stream, d_recs, batch, P,
+                     d_forces, d_status, d_iters, list1, cnt1);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
