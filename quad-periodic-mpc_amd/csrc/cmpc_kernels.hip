@@ -30,6 +30,13 @@
 
 #include "cmpc_kernels.h"
 
+// Scheduling fence for the long unrolled LDS->FMA sweeps: without it the scheduler issues all
+// 16 ds_read_b128 of a 64-wide row up front (64 extra live VGPRs on top of the 65-slot row).
+#define CMPC_SWEEP_FENCE(c) \
+  do {                      \
+    if (((c) & 15) == 12) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
 namespace cmpc {
 
 namespace {
@@ -593,6 +600,8 @@ __device__ __forceinline__ void solve_instance(const float* __restrict__ rec, co
       slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
       slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
       slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+
+      CMPC_SWEEP_FENCE(c);
     }
     slot[NV] = fmaf(a, Mk[NV], slot[NV]);
   }
@@ -619,6 +628,8 @@ __device__ __forceinline__ void solve_instance(const float* __restrict__ rec, co
       slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
       slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
       slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+
+      CMPC_SWEEP_FENCE(c);
     }
   }
   {
@@ -638,6 +649,7 @@ __device__ __forceinline__ void solve_instance(const float* __restrict__ rec, co
     xv = fmaf(slot[c + 1], y4.y, xv);
     xv = fmaf(slot[c + 2], y4.z, xv);
     xv = fmaf(slot[c + 3], y4.w, xv);
+    CMPC_SWEEP_FENCE(c);
   }
   xv = -xv;
   if (v >= n) xv = 0.f;
@@ -929,6 +941,8 @@ __device__ __forceinline__ float chol_w1(float (&slot)[65], int n, SharedW1& sh,
         slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
         slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
         slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+
+        CMPC_SWEEP_FENCE(c);
       }
       slot[NV] = fmaf(a, buf[NV], slot[NV]);
     }
@@ -952,28 +966,28 @@ __device__ __forceinline__ void inv_w1(float (&slot)[65], int n, SharedW1& sh) {
     if (l < n) {
       const float inv_l = 1.f / rl(slot[l], l);
       float* buf = sh.bufA[l & 1];
+      // lane l publishes its raw accumulator row (zeros below its diagonal, d_l on it)
       if (lane_eq(l)) {
 #pragma unroll
-        for (int c = c0; c < NV; c += 4) {
-          float w4[4];
-#pragma unroll
-          for (int t = 0; t < 4; t++) {
-            const int cc = c + t;
-            w4[t] = (cc < l) ? 0.f : ((cc == l) ? inv_l - 1.f : -slot[cc] * inv_l);
-          }
-          *reinterpret_cast<float4*>(&buf[c]) = make_float4(w4[0], w4[1], w4[2], w4[3]);
-        }
+        for (int c = c0; c < NV; c += 4)
+          *reinterpret_cast<float4*>(&buf[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
       }
       wsync();
+      // rows i < l: acc_i += U[i][l] X[l] with X[l] = -raw_l * inv_l off the diagonal and
+      // X[l][l] = inv_l; slot[l] (which held U[i][l]) becomes U[i][l] * inv_l
       const float u = lane_lt(l) ? slot[l] : 0.f;
+      const float a = -u * inv_l;
 #pragma unroll
       for (int c = c0; c < NV; c += 4) {
         const float4 r4 = *reinterpret_cast<const float4*>(&buf[c]);
-        slot[c + 0] = fmaf(u, r4.x, slot[c + 0]);
-        slot[c + 1] = fmaf(u, r4.y, slot[c + 1]);
-        slot[c + 2] = fmaf(u, r4.z, slot[c + 2]);
-        slot[c + 3] = fmaf(u, r4.w, slot[c + 3]);
+        slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
+        slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
+        slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
+        slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+
+        CMPC_SWEEP_FENCE(c);
       }
+      slot[l] = fmaf(u, inv_l, slot[l]);
       // lane l finalises its row (branch-free: a divergent branch here would force the register
       // allocator to keep two copies of the row live)
       const float fl = wl(-inv_l, l, 1.f);
@@ -989,6 +1003,7 @@ __device__ __forceinline__ void inv_w1(float (&slot)[65], int n, SharedW1& sh) {
 __device__ __forceinline__ float xsol_w1(const float (&slot)[65], int n, float yv, SharedW1& sh) {
   constexpr int NV = 64;
   const int v = threadIdx.x;
+  (void)v;
   // ---- unconstrained minimiser x = -J y -----------------------------------------------------
   sh.dfull[v] = yv;
   wsync();
@@ -1000,6 +1015,7 @@ __device__ __forceinline__ float xsol_w1(const float (&slot)[65], int n, float y
     xv = fmaf(slot[c + 1], y4.y, xv);
     xv = fmaf(slot[c + 2], y4.z, xv);
     xv = fmaf(slot[c + 3], y4.w, xv);
+    CMPC_SWEEP_FENCE(c);
   }
   xv = (v < n) ? -xv : 0.f;
   wsync();
@@ -1051,20 +1067,20 @@ __device__ __forceinline__ int gi_w1(float (&slot)[65], float& xv, int n, int nf
       for (;;) {
         if (++iters > cap) { status = CMPC_MAX_ITER; break; }
         // d = J' n+  (rows ia, iz of J through LDS)
+        // raw rows only: any arithmetic inside these divergent stores gets speculated by the
+        // compiler for all 64 slots (64 extra live registers)
         if (v == cp.ia) {
 #pragma unroll
           for (int c = 0; c < NV; c += 4)
-            *reinterpret_cast<float4*>(&sh.bufA[0][c]) =
-                make_float4(cp.ca * slot[c], cp.ca * slot[c + 1], cp.ca * slot[c + 2], cp.ca * slot[c + 3]);
+            *reinterpret_cast<float4*>(&sh.bufA[0][c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
         }
         if (v == cp.iz) {
 #pragma unroll
           for (int c = 0; c < NV; c += 4)
-            *reinterpret_cast<float4*>(&sh.bufB[c]) =
-                make_float4(cp.cb * slot[c], cp.cb * slot[c + 1], cp.cb * slot[c + 2], cp.cb * slot[c + 3]);
+            *reinterpret_cast<float4*>(&sh.bufB[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
         }
         wsync();
-        const float dv = sh.bufA[0][v] + sh.bufB[v];
+        const float dv = fmaf(cp.ca, sh.bufA[0][v], cp.cb * sh.bufB[v]);
         sh.dfull[v] = dv;
         sh.dmask[v] = (v >= q) ? dv : 0.f;
         wsync();
@@ -1222,7 +1238,10 @@ __global__ __launch_bounds__(64 * W) void cmpc_solve_kernel(
   }
 }
 
-__global__ __launch_bounds__(64) void cmpc_solve_w1_kernel(
+#ifndef CMPC_W1_WAVES_PER_EU
+#define CMPC_W1_WAVES_PER_EU 2  // 2 waves/SIMD: measured best (r01: 6.1 ms vs 10.2 at 1, 9.5 at 3 with spills)
+#endif
+__global__ __launch_bounds__(64, CMPC_W1_WAVES_PER_EU) void cmpc_solve_w1_kernel(
     const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
     uint8_t* __restrict__ status, int32_t* __restrict__ iters, int* __restrict__ ovf_list,
     int* __restrict__ ovf_count) {

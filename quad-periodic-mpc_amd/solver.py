@@ -22,7 +22,7 @@ import numpy as np
 from .records import CmpcParams, make_params, record_words
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libcmpc_hip.so")
+LIB_PATH = os.environ.get("CMPC_LIB", os.path.join(PKG, "libcmpc_hip.so"))
 
 # every symbol include/cmpc_solver.h declares (C linkage unless noted)
 EXPORTED_SYMBOLS = (
