@@ -1,3 +1,4 @@
+#pragma once
 // cmpc_kernels.hip — fused condensation + friction-cone QP, one MPC instance per workgroup.
 //
 // What one workgroup computes is one call of the reference's solve_mpc()
@@ -29,6 +30,8 @@
 #include <type_traits>
 
 #include "cmpc_kernels.h"
+
+// Device-side solver code shared by the per-class translation units (cmpc_class*.hip).
 
 // Scheduling fence for the long unrolled LDS->FMA sweeps: without it the scheduler issues all
 // 16 ds_read_b128 of a 64-wide row up front (64 extra live VGPRs on top of the 65-slot row).
@@ -104,7 +107,6 @@ struct SharedCommon {
 };
 
 // The 64-lane class keeps U, J and the QP's R implicitly in registers: only the common part.
-struct SharedW1 : SharedCommon<64> {};
 
 // Wider classes keep the raw Cholesky rows / the QP's R explicitly in LDS (region M).
 template <int W>
@@ -910,21 +912,55 @@ __device__ __forceinline__ Cons decode_cons(int c, float mui, const float* sub) 
   return k;
 }
 
-// Bordered Cholesky [H | g] = U'[U | y] (lane v: row v). Returns y_v; slot <- U row v with
+// ---------------------------------------------------------------------------------------------
+// Register-resident solver for W wavefronts (NV = 64 W rows, thread v owns row v).
+// W = 1 uses cross-lane readlane/DPP-free shuffles; W > 1 exchanges through LDS + s_barrier.
+// ---------------------------------------------------------------------------------------------
+template <int W>
+struct SharedReg : SharedCommon<64 * W> {
+  static constexpr int NVR = 64 * W;
+  float u[NVR + 4];        // duals of the active set
+  int act[NVR + 4];        // active constraint ids
+  float rvec[NVR + 4];     // dual step r
+  float tsv[NVR + 4];      // suffix norms
+  float cs[2 * NVR + 8];   // Givens (c, s)
+  float xch[8];            // cross-wave scalar exchange
+};
+
+template <int W>
+__device__ __forceinline__ void bar() {
+  if constexpr (W == 1) wsync();
+  else __syncthreads();
+}
+
+// value of register x held by thread `row` (uniform row index), for every thread
+template <int W>
+__device__ __forceinline__ void row_vals2(float x0, float x1, int row, SharedReg<W>& sh, float& y0,
+                                          float& y1) {
+  if constexpr (W == 1) {
+    y0 = rl(x0, row);
+    y1 = rl(x1, row);
+  } else {
+    if ((int)threadIdx.x == row) { sh.xch[0] = x0; sh.xch[1] = x1; }
+    __syncthreads();
+    y0 = sh.xch[0];
+    y1 = sh.xch[1];
+    __syncthreads();
+  }
+}
+
+// Bordered Cholesky [H | g] = U'[U | y] (thread v: row v). Returns y_v; slot <- U row v with
 // zeros below the diagonal.
-__device__ __forceinline__ float chol_w1(float (&slot)[65], int n, SharedW1& sh, int& status) {
-  constexpr int NV = 64;
+template <int W>
+__device__ __forceinline__ float chol_reg(float (&slot)[64 * W + 1], int n, SharedReg<W>& sh,
+                                          int& status) {
+  constexpr int NV = 64 * W;
   const int v = threadIdx.x;
-  // ---- bordered Cholesky [H | g] = U'[U | y], right-looking, pivot row k broadcast via LDS --
   float my_inv = 1.f;
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int c0 = k & ~3;
     if (k < n) {
-      float d2 = rl(slot[k], k);
-      if (!(d2 > 0.f)) { status = CMPC_NOT_PD; d2 = 1e-30f; }
-      const float inv = rsqrtf(d2);
-      my_inv = wl(inv, k, my_inv);
       float* buf = sh.bufA[k & 1];
       if (lane_eq(k)) {
 #pragma unroll
@@ -932,7 +968,11 @@ __device__ __forceinline__ float chol_w1(float (&slot)[65], int n, SharedW1& sh,
           *reinterpret_cast<float4*>(&buf[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
         buf[NV] = slot[NV];
       }
-      wsync();
+      bar<W>();
+      float d2 = buf[k];
+      if (!(d2 > 0.f)) { status = CMPC_NOT_PD; d2 = 1e-30f; }
+      const float inv = rsqrtf(d2);
+      my_inv = wl(inv, k, my_inv);
       const float a = lane_gt(k) ? -buf[v] * inv * inv : 0.f;
 #pragma unroll
       for (int c = c0; c < NV; c += 4) {
@@ -941,7 +981,6 @@ __device__ __forceinline__ float chol_w1(float (&slot)[65], int n, SharedW1& sh,
         slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
         slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
         slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
-
         CMPC_SWEEP_FENCE(c);
       }
       slot[NV] = fmaf(a, buf[NV], slot[NV]);
@@ -951,28 +990,26 @@ __device__ __forceinline__ float chol_w1(float (&slot)[65], int n, SharedW1& sh,
   const float yv = slot[NV] * my_inv;
 #pragma unroll
   for (int c = 0; c < NV; c++) slot[c] = (c < v) ? 0.f : slot[c] * my_inv;
-
   return yv;
 }
 
-// J = U^{-1} in place (lane v: row v of J).
-__device__ __forceinline__ void inv_w1(float (&slot)[65], int n, SharedW1& sh) {
-  constexpr int NV = 64;
-  const int v = threadIdx.x;
-  // ---- J = U^{-1} in place, rows l descending (in-place scheme: DESIGN.md) ------------------
+// J = U^{-1} in place (thread v: row v of J), rows l descending (in-place scheme).
+template <int W>
+__device__ __forceinline__ void inv_reg(float (&slot)[64 * W + 1], int n, SharedReg<W>& sh) {
+  constexpr int NV = 64 * W;
   static_for<0, NV>([&](auto IC) {
     constexpr int l = NV - 1 - decltype(IC)::value;
     constexpr int c0 = l & ~3;
     if (l < n) {
-      const float inv_l = 1.f / rl(slot[l], l);
       float* buf = sh.bufA[l & 1];
-      // lane l publishes its raw accumulator row (zeros below its diagonal, d_l on it)
+      // row l publishes its raw accumulator row (zeros below its diagonal, d_l on it)
       if (lane_eq(l)) {
 #pragma unroll
         for (int c = c0; c < NV; c += 4)
           *reinterpret_cast<float4*>(&buf[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
       }
-      wsync();
+      bar<W>();
+      const float inv_l = 1.f / buf[l];
       // rows i < l: acc_i += U[i][l] X[l] with X[l] = -raw_l * inv_l off the diagonal and
       // X[l][l] = inv_l; slot[l] (which held U[i][l]) becomes U[i][l] * inv_l
       const float u = lane_lt(l) ? slot[l] : 0.f;
@@ -984,29 +1021,26 @@ __device__ __forceinline__ void inv_w1(float (&slot)[65], int n, SharedW1& sh) {
         slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
         slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
         slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
-
         CMPC_SWEEP_FENCE(c);
       }
       slot[l] = fmaf(u, inv_l, slot[l]);
-      // lane l finalises its row (branch-free: a divergent branch here would force the register
-      // allocator to keep two copies of the row live)
+      // row l finalises itself (branch-free)
       const float fl = wl(-inv_l, l, 1.f);
 #pragma unroll
       for (int c = l + 1; c < NV; c++) slot[c] *= fl;
       slot[l] = wl(inv_l, l, slot[l]);
     }
   });
-
 }
 
-// Unconstrained minimiser x = -J y (lane v: x_v).
-__device__ __forceinline__ float xsol_w1(const float (&slot)[65], int n, float yv, SharedW1& sh) {
-  constexpr int NV = 64;
+// Unconstrained minimiser x = -J y (thread v: x_v).
+template <int W>
+__device__ __forceinline__ float xsol_reg(const float (&slot)[64 * W + 1], int n, float yv,
+                                          SharedReg<W>& sh) {
+  constexpr int NV = 64 * W;
   const int v = threadIdx.x;
-  (void)v;
-  // ---- unconstrained minimiser x = -J y -----------------------------------------------------
   sh.dfull[v] = yv;
-  wsync();
+  bar<W>();
   float xv = 0.f;
 #pragma unroll
   for (int c = 0; c < NV; c += 4) {
@@ -1018,197 +1052,226 @@ __device__ __forceinline__ float xsol_w1(const float (&slot)[65], int n, float y
     CMPC_SWEEP_FENCE(c);
   }
   xv = (v < n) ? -xv : 0.f;
-  wsync();
-
+  bar<W>();
   return xv;
 }
 
-// Goldfarb-Idnani on the friction pyramids; J in slot (updated), x in xv. Returns iterations.
-__device__ __forceinline__ int gi_w1(float (&slot)[65], float& xv, int n, int nfs, const KParams& P,
-                                     SharedW1& sh, int& status) {
-  constexpr int NV = 64;
+// Goldfarb-Idnani dual active set on the friction pyramids with R implicit:
+// R[i][j] = J[:,i]' n_j recomputed from J (registers) and the 2-sparse normals n_j.
+template <int W>
+__device__ __forceinline__ int gi_reg(float (&slot)[64 * W + 1], float& xv, int n, int nfs,
+                                      const KParams& P, SharedReg<W>& sh, int& status) {
+  constexpr int NV = 64 * W;
+  constexpr int NT = 64 * W;
   const int v = threadIdx.x;
-  // ---- Goldfarb-Idnani dual active set, R implicit ----------------------------------------
   const float mui = P.mu_inv;
   const float fnorm = 1.f / sqrtf(mui * mui + 1.f);
-  int q = 0;            // active-set size (uniform)
-  int act_v = 0;        // lane j < q: id of the j-th active constraint
-  float u_v = 0.f;      // lane j < q: its dual
+  int q = 0;
   int iters = 0;
   const int cap = P.max_iter;
-  if (status == CMPC_OK) {
-    for (;;) {
-      sh.xs[v] = xv;
-      wsync();
-      float best = 0.f;
-      int bid = 0x7fffffff;
-      if (v < nfs) {
-        const int s = v;
-        const float fx = sh.xs[3 * s], fy = sh.xs[3 * s + 1], fz = sh.xs[3 * s + 2];
-        float sl[6];
-        sl[0] = (mui * fx + fz) * fnorm;
-        sl[1] = (-mui * fx + fz) * fnorm;
-        sl[2] = (mui * fy + fz) * fnorm;
-        sl[3] = (-mui * fy + fz) * fnorm;
-        sl[4] = fz;
-        sl[5] = sh.sub[s] - fz;
+  if (status != CMPC_OK) return 0;
+  for (;;) {
+    sh.xs[v] = xv;
+    bar<W>();
+    float best = 0.f;
+    int bid = 0x7fffffff;
+    for (int s = v; s < nfs; s += NT) {
+      const float fx = sh.xs[3 * s], fy = sh.xs[3 * s + 1], fz = sh.xs[3 * s + 2];
+      float sl[6];
+      sl[0] = (mui * fx + fz) * fnorm;
+      sl[1] = (-mui * fx + fz) * fnorm;
+      sl[2] = (mui * fy + fz) * fnorm;
+      sl[3] = (-mui * fy + fz) * fnorm;
+      sl[4] = fz;
+      sl[5] = sh.sub[s] - fz;
 #pragma unroll
-        for (int t = 0; t < 6; t++)
-          if (!sh.cflag[6 * s + t] && sl[t] < best) { best = sl[t]; bid = 6 * s + t; }
-      }
-      const float xmax = wave_max(fabsf(xv));
-      wave_argmin(best, bid);
-      const float tol = 1e-5f * fmaxf(1.f, xmax);
-      if (bid == 0x7fffffff || best >= -tol) break;
+      for (int t = 0; t < 6; t++)
+        if (!sh.cflag[6 * s + t] && sl[t] < best) { best = sl[t]; bid = 6 * s + t; }
+    }
+    const float xmax = block_max<W>(fabsf(xv), sh);
+    block_argmin<W>(best, bid, sh);
+    const float tol = 1e-5f * fmaxf(1.f, xmax);
+    if (bid == 0x7fffffff || best >= -tol) break;
 
-      const int p = __builtin_amdgcn_readfirstlane(bid);
-      const Cons cp = decode_cons(p, mui, sh.sub);
-      float up = 0.f;
-      for (;;) {
-        if (++iters > cap) { status = CMPC_MAX_ITER; break; }
-        // d = J' n+  (rows ia, iz of J through LDS)
-        // raw rows only: any arithmetic inside these divergent stores gets speculated by the
-        // compiler for all 64 slots (64 extra live registers)
-        if (v == cp.ia) {
+    const int p = __builtin_amdgcn_readfirstlane(bid);
+    const Cons cp = decode_cons(p, mui, sh.sub);
+    float up = 0.f;
+    for (;;) {
+      if (++iters > cap) { status = CMPC_MAX_ITER; break; }
+      // d = J' n+ (raw rows ia, iz through LDS; no arithmetic inside the divergent stores)
+      if (v == cp.ia) {
 #pragma unroll
-          for (int c = 0; c < NV; c += 4)
-            *reinterpret_cast<float4*>(&sh.bufA[0][c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
-        }
-        if (v == cp.iz) {
+        for (int c = 0; c < NV; c += 4)
+          *reinterpret_cast<float4*>(&sh.bufA[0][c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
+      }
+      if (v == cp.iz) {
 #pragma unroll
-          for (int c = 0; c < NV; c += 4)
-            *reinterpret_cast<float4*>(&sh.bufB[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
-        }
-        wsync();
-        const float dv = fmaf(cp.ca, sh.bufA[0][v], cp.cb * sh.bufB[v]);
-        sh.dfull[v] = dv;
-        sh.dmask[v] = (v >= q) ? dv : 0.f;
-        wsync();
-        // z = J2 d2, zn = |d2|^2 (= z' n+), dn = |d|^2
-        float zv = 0.f, zn = 0.f, dn = 0.f;
+        for (int c = 0; c < NV; c += 4)
+          *reinterpret_cast<float4*>(&sh.bufB[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
+      }
+      bar<W>();
+      const float dv = fmaf(cp.ca, sh.bufA[0][v], cp.cb * sh.bufB[v]);
+      sh.dfull[v] = dv;
+      sh.dmask[v] = (v >= q) ? dv : 0.f;
+      bar<W>();
+      // z = J2 d2, zn = |d2|^2 (= z' n+), dn = |d|^2
+      float zv = 0.f, zn = 0.f, dn = 0.f;
 #pragma unroll
-        for (int c = 0; c < NV; c += 4) {
-          const float4 m4 = *reinterpret_cast<const float4*>(&sh.dmask[c]);
-          const float4 f4 = *reinterpret_cast<const float4*>(&sh.dfull[c]);
-          zv = fmaf(slot[c + 0], m4.x, zv);
-          zv = fmaf(slot[c + 1], m4.y, zv);
-          zv = fmaf(slot[c + 2], m4.z, zv);
-          zv = fmaf(slot[c + 3], m4.w, zv);
-          zn += m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
-          dn += f4.x * f4.x + f4.y * f4.y + f4.z * f4.z + f4.w * f4.w;
-        }
-        // r = R^{-1} d1 with R[i][j] = J[:,i]' n_j: back substitution through the vector
-        // m = sum_{j>i} r_j n_j, so sum_{j>i} R[i][j] r_j = J[:,i]' m (one column dot per i)
-        float m = 0.f, rv = 0.f;
-        static_for<0, NV>([&](auto IC) {
-          constexpr int i = NV - 1 - decltype(IC)::value;
-          if (i < q) {
-            const Cons ci = decode_cons(rli(act_v, opaque(i)), mui, sh.sub);
-            const float Rii = ci.ca * rl(slot[i], ci.ia) + ci.cb * rl(slot[i], ci.iz);
-            const float sdot = wave_sum(slot[i] * m);
-            const float ri = (rl(dv, i) - sdot) / Rii;
-            rv = wl(ri, i, rv);
-            m = wl(fmaf(ci.ca, ri, rl(m, ci.ia)), ci.ia, m);
-            m = wl(fmaf(ci.cb, ri, rl(m, ci.iz)), ci.iz, m);
+      for (int c = 0; c < NV; c += 4) {
+        const float4 m4 = *reinterpret_cast<const float4*>(&sh.dmask[c]);
+        const float4 f4 = *reinterpret_cast<const float4*>(&sh.dfull[c]);
+        zv = fmaf(slot[c + 0], m4.x, zv);
+        zv = fmaf(slot[c + 1], m4.y, zv);
+        zv = fmaf(slot[c + 2], m4.z, zv);
+        zv = fmaf(slot[c + 3], m4.w, zv);
+        zn += m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
+        dn += f4.x * f4.x + f4.y * f4.y + f4.z * f4.z + f4.w * f4.w;
+        CMPC_SWEEP_FENCE(c);
+      }
+      // r = R^{-1} d1: back substitution through m = sum_{j>i} r_j n_j
+      // (sum_{j>i} R[i][j] r_j = J[:,i]' m: one column dot per i)
+      float m = 0.f;
+      static_for<0, NV>([&](auto IC) {
+        constexpr int i = NV - 1 - decltype(IC)::value;
+        if (i < q) {
+          const Cons ci = decode_cons(sh.act[opaque(i)], mui, sh.sub);
+          float ja, jz;
+          row_vals2<W>(slot[i], slot[i], ci.ia, sh, ja, jz);
+          if (ci.iz != ci.ia) {
+            float t0;
+            row_vals2<W>(slot[i], slot[i], ci.iz, sh, jz, t0);
           }
-        });
-        // partial (dual) step t1 and full (primal) step t2
-        float t1 = kBigF;
-        int kk = 0x7fffffff;
-        if (v < q && rv > 0.f) { t1 = fmaxf(u_v / rv, 0.f); kk = v; }
-        wave_argmin(t1, kk);
-        const float spv = fmaf(cp.ca, rl(xv, cp.ia), fmaf(cp.cb, rl(xv, cp.iz), -cp.bp));
-        const bool zero_step = !(zn > 1e-9f * dn);
-        const float t2 = zero_step ? kBigF : -spv / zn;
-        const float t = fminf(t1, t2);
-        if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
-        if (v < q) u_v = fmaf(-t, rv, u_v);
-        up += t;
-        if (!zero_step) xv = fmaf(t, zv, xv);
-        if (!zero_step && t2 <= t1) {
-          // ---- add p: Givens zeroing d[q+1..n-1] into d[q]; params from suffix norms ----
-          const float dsq = (v >= q && v < n) ? dv * dv : 0.f;
-          const float ts = sqrtf(wave_suffix_sum(dsq, v));
-          const float ts_prev = __shfl_up(ts, 1, 64);
-          const float d_prev = __shfl_up(dv, 1, 64);
+          const float Rii = fmaf(ci.ca, ja, ci.cb * jz);
+          const float sdot = block_sum<W>(slot[i] * m, sh);
+          const float ri = (sh.dfull[i] - sdot) / Rii;
+          if (v == 0) sh.rvec[i] = ri;
+          if (v == ci.ia) m = fmaf(ci.ca, ri, m);
+          if (v == ci.iz) m = fmaf(ci.cb, ri, m);
+        }
+      });
+      bar<W>();
+      // partial (dual) step t1 and full (primal) step t2
+      float t1 = kBigF;
+      int kk = 0x7fffffff;
+      if (v < q) {
+        const float rj = sh.rvec[v];
+        if (rj > 0.f) { t1 = fmaxf(sh.u[v] / rj, 0.f); kk = v; }
+      }
+      block_argmin<W>(t1, kk, sh);
+      const float spv = fmaf(cp.ca, sh.xs[cp.ia], fmaf(cp.cb, sh.xs[cp.iz], -cp.bp));
+      const bool zero_step = !(zn > 1e-9f * dn);
+      const float t2 = zero_step ? kBigF : -spv / zn;
+      const float t = fminf(t1, t2);
+      if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
+      if (v < q) sh.u[v] = fmaf(-t, sh.rvec[v], sh.u[v]);
+      up += t;
+      if (!zero_step) {
+        xv = fmaf(t, zv, xv);
+        sh.xs[v] = xv;
+      }
+      bar<W>();
+      if (!zero_step && t2 <= t1) {
+        // ---- add p: Givens zeroing d[q+1..n-1] into d[q]; params from suffix norms ----
+        const float dsq = (v >= q && v < n) ? dv * dv : 0.f;
+        const float ts = sqrtf(block_suffix_sum<W>(dsq, sh));
+        sh.tsv[v] = ts;
+        bar<W>();
+        if (v > q && v < n) {
+          const float ts_prev = sh.tsv[v - 1];
           float cj = 1.f, sj = 0.f;
-          if (v > q && v < n && ts_prev > 0.f) {
-            cj = d_prev / ts_prev;
+          if (ts_prev > 0.f) {
+            cj = sh.dfull[v - 1] / ts_prev;
             sj = ((v == n - 1) ? dv : ts) / ts_prev;
           }
-          static_for<0, NV - 1>([&](auto IC) {
-            constexpr int j = NV - 1 - decltype(IC)::value;  // 63 .. 1
-            if ((unsigned)(j - q - 1) < (unsigned)(n - q - 1)) {  // q < j < n, not hoistable
-              const int jj = opaque(j);
-              const float c = rl(cj, jj), sn = rl(sj, jj);
-              const float a0 = slot[j - 1], b0 = slot[j];
-              slot[j - 1] = fmaf(c, a0, sn * b0);
-              slot[j] = fmaf(-sn, a0, c * b0);
-            }
-          });
-          act_v = wli(p, q, act_v);
-          u_v = wl(up, q, u_v);
-          if (v == 0) sh.cflag[p] = 1;
-          q++;
-          break;
+          sh.cs[2 * v] = cj;
+          sh.cs[2 * v + 1] = sj;
         }
-        // ---- drop active constraint kk, then re-triangularise (implicit R) ----------------
-        {
-          const int k = __builtin_amdgcn_readfirstlane(kk);
-          const int dropped = rli(act_v, k);
-          if (v == 0) sh.cflag[dropped] = 0;
-          const int a_nx = __shfl_down(act_v, 1, 64);
-          const float u_nx = __shfl_down(u_v, 1, 64);
-          if (v >= k && v < q - 1) { act_v = a_nx; u_v = u_nx; }
-          static_for<0, NV - 1>([&](auto JC) {
-            constexpr int j = decltype(JC)::value;  // 0 .. 62
-            if (j >= k && j < q - 1) {
-              const Cons cj2 = decode_cons(rli(act_v, opaque(j)), mui, sh.sub);
-              const float a0 = cj2.ca * rl(slot[j], cj2.ia) + cj2.cb * rl(slot[j], cj2.iz);
-              const float b0 = cj2.ca * rl(slot[j + 1], cj2.ia) + cj2.cb * rl(slot[j + 1], cj2.iz);
-              const float h = sqrtf(a0 * a0 + b0 * b0);
-              float c = 1.f, sn = 0.f;
-              if (h > 0.f) { c = a0 / h; sn = b0 / h; }
-              const float x0 = slot[j], x1 = slot[j + 1];
-              slot[j] = fmaf(c, x0, sn * x1);
-              slot[j + 1] = fmaf(-sn, x0, c * x1);
-            }
-          });
-          q--;
+        if (v == 0) {
+          sh.act[q] = p;
+          sh.u[q] = up;
+          sh.cflag[p] = 1;
         }
+        bar<W>();
+        static_for<0, NV - 1>([&](auto IC) {
+          constexpr int j = NV - 1 - decltype(IC)::value;  // NV-1 .. 1
+          if ((unsigned)(j - q - 1) < (unsigned)(n - q - 1)) {  // q < j < n
+            const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * opaque(j)]);
+            const float a0 = slot[j - 1], b0 = slot[j];
+            slot[j - 1] = fmaf(cs2.x, a0, cs2.y * b0);
+            slot[j] = fmaf(-cs2.y, a0, cs2.x * b0);
+          }
+        });
+        q++;
+        bar<W>();
+        break;
       }
-      if (status != CMPC_OK) break;
+      // ---- drop active constraint kk, then re-triangularise (implicit R) ----------------
+      {
+        const int k = __builtin_amdgcn_readfirstlane(kk);
+        int a_nx = 0;
+        float u_nx = 0.f;
+        if (v >= k && v < q - 1) { a_nx = sh.act[v + 1]; u_nx = sh.u[v + 1]; }
+        if (v == 0) sh.cflag[sh.act[k]] = 0;
+        bar<W>();
+        if (v >= k && v < q - 1) { sh.act[v] = a_nx; sh.u[v] = u_nx; }
+        bar<W>();
+        static_for<0, NV - 1>([&](auto JC) {
+          constexpr int j = decltype(JC)::value;  // 0 .. NV-2
+          if ((unsigned)(j - k) < (unsigned)(q - 1 - k)) {  // k <= j < q-1
+            const Cons cj2 = decode_cons(sh.act[opaque(j)], mui, sh.sub);
+            float aa0, aa1, zz0, zz1;
+            row_vals2<W>(slot[j], slot[j + 1], cj2.ia, sh, aa0, aa1);
+            row_vals2<W>(slot[j], slot[j + 1], cj2.iz, sh, zz0, zz1);
+            const float a0 = fmaf(cj2.ca, aa0, cj2.cb * zz0);
+            const float b0 = fmaf(cj2.ca, aa1, cj2.cb * zz1);
+            const float h = sqrtf(a0 * a0 + b0 * b0);
+            float c = 1.f, sn = 0.f;
+            if (h > 0.f) { c = a0 / h; sn = b0 / h; }
+            const float x0 = slot[j], x1 = slot[j + 1];
+            slot[j] = fmaf(c, x0, sn * x1);
+            slot[j + 1] = fmaf(-sn, x0, c * x1);
+          }
+        });
+        q--;
+      }
     }
+    if (status != CMPC_OK) break;
   }
-
   return iters;
 }
 
-__device__ __forceinline__ void solve_w1(const float* __restrict__ rec, const KParams& P, SharedW1& sh,
-                         float* __restrict__ fout, uint8_t* __restrict__ st_out,
-                         int32_t* __restrict__ it_out, int* __restrict__ ovf_list,
-                         int* __restrict__ ovf_count, int inst) {
-  constexpr int NV = 64;
+template <int W>
+__device__ __forceinline__ void solve_reg(const float* __restrict__ rec, const KParams& P,
+                                          SharedReg<W>& sh, float* __restrict__ fout,
+                                          uint8_t* __restrict__ st_out, int32_t* __restrict__ it_out,
+                                          int* __restrict__ ovf_list, int* __restrict__ ovf_count,
+                                          int inst) {
+  constexpr int NV = 64 * W;
+  constexpr int NT = 64 * W;
   const int v = threadIdx.x;
   const int N = P.N;
   float slot[NV + 1];
   int nfs = 0;
-  const int n = prepare_instance<1>(rec, P, sh, false, slot, nfs);
+  const int n = prepare_instance<W>(rec, P, sh, false, slot, nfs);
   if (n > NV) {
-    if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
+    if (ovf_list != nullptr) {  // hand the instance to the next size class
+      if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
+      return;
+    }
+    for (int t = v; t < 12 * N; t += NT) fout[t] = 0.f;  // no wider class available
+    if (v == 0) { st_out[0] = CMPC_BAD_INPUT; if (it_out) it_out[0] = 0; }
     return;
   }
-
   int status = CMPC_OK;
-  const float yv = chol_w1(slot, n, sh, status);
-  inv_w1(slot, n, sh);
-  float xv = xsol_w1(slot, n, yv, sh);
-  const int iters = gi_w1(slot, xv, n, nfs, P, sh, status);
+  const float yv = chol_reg<W>(slot, n, sh, status);
+  inv_reg<W>(slot, n, sh);
+  float xv = xsol_reg<W>(slot, n, yv, sh);
+  const int iters = gi_reg<W>(slot, xv, n, nfs, P, sh, status);
 
   // ---- scatter forces (q_soln layout: 12 k + 3 leg + axis; swing -> 0) --------------------
   const bool ok = (status == CMPC_OK);
   if (v < n) fout[12 * sh.varblk[v] + sh.varcol[v]] = ok ? xv : 0.f;
-  for (int t = v; t < 12 * N; t += NV)
+  for (int t = v; t < 12 * N; t += NT)
     if (!sh.stance[t / 3] || !ok) fout[t] = 0.f;
   if (v == 0) {
     st_out[0] = (uint8_t)status;
@@ -1217,94 +1280,5 @@ __device__ __forceinline__ void solve_w1(const float* __restrict__ rec, const KP
 }
 
 }  // namespace
-
-// ---------------------------------------------------------------------------------------------
-// Kernels. The first size class runs one workgroup per instance over the whole batch; larger
-// classes run a persistent grid over the overflow list filled by the previous class.
-// ---------------------------------------------------------------------------------------------
-template <int W>
-__global__ __launch_bounds__(64 * W) void cmpc_solve_kernel(
-    const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
-    uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
-    const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
-  __shared__ Shared<W> sh;
-  const int count = in_list ? *in_count : batch;
-  for (int t = blockIdx.x; t < count; t += gridDim.x) {
-    const int inst = in_list ? in_list[t] : t;
-    solve_instance<W>(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
-                      status + inst, iters ? iters + inst : nullptr, ovf_list, ovf_count, inst,
-                      nullptr, nullptr);
-    __syncthreads();
-  }
-}
-
-#ifndef CMPC_W1_WAVES_PER_EU
-#define CMPC_W1_WAVES_PER_EU 2  // 2 waves/SIMD: measured best (r01: 6.1 ms vs 10.2 at 1, 9.5 at 3 with spills)
-#endif
-__global__ __launch_bounds__(64, CMPC_W1_WAVES_PER_EU) void cmpc_solve_w1_kernel(
-    const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
-    uint8_t* __restrict__ status, int32_t* __restrict__ iters, int* __restrict__ ovf_list,
-    int* __restrict__ ovf_count) {
-  __shared__ SharedW1 sh;
-  const int inst = blockIdx.x;
-  if (inst >= batch) return;
-  solve_w1(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N, status + inst,
-           iters ? iters + inst : nullptr, ovf_list, ovf_count, inst);
-}
-
-template <int W>
-__global__ __launch_bounds__(64 * W) void cmpc_condense_kernel(const float* __restrict__ recs,
-                                                               int batch, KParams P,
-                                                               float* __restrict__ H,
-                                                               float* __restrict__ g) {
-  __shared__ Shared<W> sh;
-  const int nv = 12 * P.N;
-  for (int inst = blockIdx.x; inst < batch; inst += gridDim.x) {
-    solve_instance<W>(recs + (size_t)inst * P.rec_words, P, sh, nullptr, nullptr, nullptr, nullptr,
-                      nullptr, inst, H + (size_t)inst * nv * nv, g + (size_t)inst * nv);
-    __syncthreads();
-  }
-}
-
-hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
-                        uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
-                        hipStream_t stream, hipEvent_t* ev) {
-  // d_work layout: [0] overflow count of class 1, [1] of class 2, [4 ..) lists [max_batch] x 2
-  int* cnt1 = d_work;
-  int* list1 = d_work + 4;
-  hipError_t e = hipMemsetAsync(d_work, 0, 4 * sizeof(int), stream);
-  if (e != hipSuccess) return e;
-  if (batch <= 0) return hipSuccess;
-  if (ev) (void)hipEventRecord(ev[0], stream);
-  // class 1: one 64-thread workgroup per instance; instances with > 64 stance variables are
-  // appended to list1
-  hipLaunchKernelGGL(cmpc_solve_w1_kernel, dim3(batch), dim3(64), 0, stream, d_recs, batch, P,
-                     d_forces, d_status, d_iters, list1, cnt1);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (ev) (void)hipEventRecord(ev[1], stream);
-  if (12 * P.N > 64) {
-    // class 2: persistent grid of 128-thread workgroups over list1
-    const int g2 = batch < 2048 ? batch : 2048;
-    hipLaunchKernelGGL(cmpc_solve_kernel<2>, dim3(g2), dim3(128), 0, stream, d_recs, batch, P,
-                       d_forces, d_status, d_iters, list1, cnt1, nullptr, nullptr);
-    e = hipGetLastError();
-  }
-  if (ev) (void)hipEventRecord(ev[2], stream);
-  return e;
-}
-
-hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
-                           hipStream_t stream) {
-  if (batch <= 0) return hipSuccess;
-  const int nv = 12 * P.N;
-  if (nv <= 64)
-    hipLaunchKernelGGL(cmpc_condense_kernel<1>, dim3(batch), dim3(64), 0, stream, d_recs, batch, P, d_H, d_g);
-  else if (nv <= 128)
-    hipLaunchKernelGGL(cmpc_condense_kernel<2>, dim3(batch), dim3(128), 0, stream, d_recs, batch, P, d_H, d_g);
-  else
-    return hipErrorInvalidValue;  // 12N > 128 needs the 4-wave class (not built yet)
-  return hipGetLastError();
-}
 
 }  // namespace cmpc

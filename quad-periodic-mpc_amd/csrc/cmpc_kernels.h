@@ -28,6 +28,13 @@ inline size_t work_ints(int max_batch) { return 4 + 2 * (size_t)max_batch; }
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
                         hipStream_t stream, hipEvent_t* ev = nullptr);
+// per-class launchers (cmpc_class1.hip, cmpc_class2.hip)
+hipError_t launch_class1(const float* d_recs, int batch, const KParams& P, float* d_forces,
+                         uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
+                         int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
+hipError_t launch_class2(const float* d_recs, int batch, const KParams& P, float* d_forces,
+                         uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
+                         int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
 hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
                            hipStream_t stream);
 
