@@ -1,64 +1,86 @@
 """Build the HIP extension in-tree: libcmpc_hip.so (kernels + C ABI) for gfx950.
 
 Plain ``hipcc`` (no torch extension machinery): the library exposes only the C ABI of
-``include/cmpc_solver.h`` and is loaded with ctypes.
+``include/cmpc_solver.h`` and is loaded with ctypes. Each translation unit is compiled in
+parallel into ``build/obj`` and recompiled only when it or a header it includes changed (the
+fully unrolled register kernels take minutes per TU).
 """
 from __future__ import annotations
 
 import os
+import re
 import subprocess
-import tempfile
 from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcmpc_hip.so")
-# one translation unit per size class so the (large, fully unrolled) kernels compile in parallel
-SOURCES = ["cmpc_class1.hip", "cmpc_class2.hip", "cmpc_condense.hip", "cmpc_launch.hip",
+OBJ = os.path.join(ROOT, "build", "obj")
+# one translation unit per kernel family so the large unrolled kernels compile in parallel
+SOURCES = ["cmpc_class1.hip", "cmpc_class2.hip", "cmpc_classg.hip", "cmpc_launch.hip",
            "cmpc_abi.cpp"]
-HEADERS = ["cmpc_kernels.h", "cmpc_device.h", os.path.join("..", "..", "include", "cmpc_solver.h")]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _deps(path: str, seen=None) -> set:
+    """The file plus every quoted #include it pulls in, recursively."""
+    seen = set() if seen is None else seen
+    path = os.path.normpath(path)
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    for inc in re.findall(r'#include\s+"([^"]+)"', open(path).read()):
+        _deps(os.path.join(os.path.dirname(path), inc), seen)
+    return seen
+
+
+def _obj(src: str, defines: tuple) -> str:
+    tag = ("_" + "_".join(d.replace("=", "-") for d in defines)) if defines else ""
+    return os.path.join(OBJ, f"{src}{tag}.o")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None,
           defines: tuple = ()) -> str:
     lib = out or LIB
-    if not force and out is None and not _stale():
-        return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmpdir = tempfile.mkdtemp(prefix="cmpc_build_")
+    os.makedirs(OBJ, exist_ok=True)
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(tmpdir, src + ".o")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-result", *[f"-D{d}" for d in defines], "-c", os.path.join(CSRC, src),
-               "-o", obj]
+        path = os.path.join(CSRC, src)
+        obj = _obj(src, defines)
+        if not force and not _stale(obj, _deps(path)):
+            return obj
+        cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, *[f"-D{d}" for d in defines], "-c", path,
+               "-o", obj + ".tmp"]
         if src.endswith(".cpp"):
             cmd[1:1] = ["-x", "hip"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
         return obj
 
     jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, SOURCES))
+    if not force and not _stale(lib, objs):
+        return lib
     tmp = lib + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
-    subprocess.run(cmd, check=True)
+    subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs,
+                   check=True)
     os.replace(tmp, lib)
-    for o in objs:
-        os.remove(o)
-    os.rmdir(tmpdir)
     return lib
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+    print(build(force="--force" in sys.argv, verbose=True))

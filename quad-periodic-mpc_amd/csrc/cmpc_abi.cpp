@@ -34,6 +34,8 @@ struct cmpc_batch {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int* d_work = nullptr;
+  float* d_gscratch = nullptr;   // slabs of the general size class (cmpc_classg.hip)
+  size_t gscratch_floats = 0;
   // staging for the host-pointer entry point (allocated lazily, sized max_batch)
   float* d_rec = nullptr;
   float* d_forces = nullptr;
@@ -61,19 +63,29 @@ extern "C" int cmpc_record_words(int horizon) { return CMPC_REC_WORDS(horizon); 
 
 extern "C" const char* cmpc_last_error(void) { return g_last_error.c_str(); }
 
+// the general class needs 2 (12N)^2 floats per workgroup of its persistent grid
+static int ensure_gscratch(cmpc_batch* h) {
+  if (h->max_batch <= 0) return 0;
+  const size_t need = cmpc::classg_scratch_floats(h->prm.horizon, cmpc::classg_grid(h->max_batch));
+  if (need <= h->gscratch_floats) return 0;
+  if (h->d_gscratch) (void)hipFree(h->d_gscratch);
+  h->d_gscratch = nullptr;
+  h->gscratch_floats = 0;
+  hipError_t e = hipMalloc(&h->d_gscratch, need * sizeof(float));
+  if (e != hipSuccess) return fail("hipMalloc(class G scratch)", e);
+  h->gscratch_floats = need;
+  return 0;
+}
+
 extern "C" int cmpc_batch_set_params(cmpc_batch* h, const cmpc_params* prm) {
   if (!h || !prm) return -1;
   if (prm->horizon < 1 || prm->horizon > CMPC_MAX_HORIZON) {
     g_last_error = "horizon out of range";
     return -2;
   }
-  if (12 * prm->horizon > 128) {
-    g_last_error = "horizon > 10 with all legs in stance needs the 4-wave class (not built)";
-    // still accepted: instances with n > 128 reduced variables report CMPC_BAD_INPUT
-  }
   h->prm = *prm;
   h->kp = make_kparams(*prm);
-  return 0;
+  return ensure_gscratch(h);
 }
 
 extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int max_batch,
@@ -95,6 +107,7 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
   }
   e = hipMalloc(&h->d_work, sizeof(int) * cmpc::work_ints(max_batch));
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("hipMalloc(work)", e); }
+  if (int r = ensure_gscratch(h); r != 0) { cmpc_batch_destroy(h); return r; }
   *out = h;
   return 0;
 }
@@ -102,6 +115,7 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
 extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (!h) return;
   if (h->d_work) (void)hipFree(h->d_work);
+  if (h->d_gscratch) (void)hipFree(h->d_gscratch);
   if (h->d_rec) (void)hipFree(h->d_rec);
   if (h->d_forces) (void)hipFree(h->d_forces);
   if (h->d_status) (void)hipFree(h->d_status);
@@ -123,7 +137,7 @@ extern "C" int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int batch
   hipEvent_t* ev = nullptr;
   if (h->ev_steps > 0 && h->ev_next < h->ev_steps) ev = &h->ev[3 * h->ev_next++];
   hipError_t e = cmpc::launch_solve(d_records, batch, h->kp, d_forces, d_status, d_iters, h->d_work,
-                                    h->max_batch, h->stream, ev);
+                                    h->max_batch, h->d_gscratch, h->stream, ev);
   if (e != hipSuccess) return fail("launch_solve", e);
   return 0;
 }
@@ -165,7 +179,8 @@ extern "C" int cmpc_batch_read_timing(cmpc_batch* h, float* ms, int* steps_recor
 extern "C" int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int batch, float* d_H,
                                    float* d_g) {
   if (!h || batch < 0 || batch > h->max_batch) return -1;
-  hipError_t e = cmpc::launch_condense(d_records, batch, h->kp, d_H, d_g, h->stream);
+  hipError_t e = cmpc::launch_condense(d_records, batch, h->kp, d_H, d_g, h->d_gscratch,
+                                       cmpc::classg_grid(h->max_batch), h->stream);
   if (e != hipSuccess) return fail("launch_condense", e);
   return 0;
 }

@@ -1,34 +1,509 @@
-// cmpc_class1.hip — register-resident size class W=1 (n <= 64 reduced variables)
-#include "cmpc_device.h"
-
-namespace cmpc {
+// cmpc_class1.hip — the hot path: fused condensation + friction-cone QP for instances with
+// n <= 64 reduced force variables (every trot instance at N <= 10), one wavefront per instance.
+//
+// One wavefront computes one call of the reference's solve_mpc()
+// (be2r_cmpc_unitree/src/controllers/convexMPC/SolverMPC.cpp:566-982):
+//   stance table + swing elimination (SolverMPC.cpp:859-894), model + closed-form c2qp
+//   (cmpc_common.h), condensation of the reduced qH / qg (SolverMPC.cpp:806-814), the dense
+//   QP (qpOASES QProblem::init in the reference, SolverMPC.cpp:955-969) solved exactly by a
+//   Goldfarb-Idnani dual active-set method, scatter to q_soln (SolverMPC.cpp:970-982).
+//
+// MI355X mapping:
+//   * lane v owns reduced variable v: row v of H, then of the Cholesky working matrix, then
+//     row v of J = L^-T, held in 65 VGPRs (slot[0..63] + the gradient border slot[64]);
+//   * LDS holds one packed 64x64 upper-row matrix (8.5 KB): H during assembly, then the raw
+//     Cholesky columns. Because the trailing matrix of a right-looking Cholesky stays
+//     symmetric, pivot column k is "register slot[k] of every lane": ONE ds_write_b32 per step
+//     publishes it, and the broadcast reads are ds_read_b128;
+//   * J = L^-T is built column-wise from the stored L columns (lane-local updates);
+//   * the QP's triangular factor R is implicit, R[i][j] = J[:,i]' n_j, since the pyramid
+//     normals n_j are 2-sparse (readlane of two J entries);
+//   * every loop over matrix columns is unrolled at compile time, so register indices are
+//     constants; LDS traffic between lanes of the single wavefront needs no s_barrier.
+// Everything is fp32 (the reference condenses in fp32: common_types.h:14).
+#include "cmpc_common.h"
 
 #ifndef CMPC_W1_WAVES_PER_EU
-#define CMPC_W1_WAVES_PER_EU 2  // 2 waves/SIMD: measured best (r01: 6.1 ms vs 10.2 at 1, 9.5 at 3 with spills)
+#define CMPC_W1_WAVES_PER_EU 2
 #endif
-// Register-resident size classes. Class W handles instances with n <= 64 W reduced variables;
-// class 1 runs one workgroup per instance over the batch, wider classes run a persistent grid
-// over the overflow list of the previous class.
-template <int W>
-__global__ __launch_bounds__(64 * W, (W == 1 ? CMPC_W1_WAVES_PER_EU : 1)) void cmpc_solve_reg_kernel(
-    const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
-    uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
-    const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
-  __shared__ SharedReg<W> sh;
-  const int count = in_list ? *in_count : batch;
-  for (int t = blockIdx.x; t < count; t += gridDim.x) {
-    const int inst = in_list ? in_list[t] : t;
-    solve_reg<W>(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
-                 status + inst, iters ? iters + inst : nullptr, ovf_list, ovf_count, inst);
-    __syncthreads();
+
+namespace cmpc {
+namespace {
+
+constexpr int NV = 64;
+constexpr int NG = NV / 4;
+constexpr int PSZ = 4 * NG * NV - 8 * NG * (NG - 1);  // packed rows r: columns [r & ~3, NV)
+
+// offset of packed row r (16-B aligned)
+__host__ __device__ constexpr int prow(int r) {
+  return 4 * (r >> 2) * NV - 8 * (r >> 2) * ((r >> 2) - 1) + (r & 3) * (NV - 4 * (r >> 2));
+}
+// prow(r) - (r & ~3): element (r, c) lives at prow0(r) + c
+__host__ __device__ constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+
+// prep scratch inside P (P is not yet holding H while these are live)
+constexpr int OFF_TRAJ = 0;
+constexpr int OFF_E = 12 * MAXN;
+constexpr int OFF_ZE = OFF_E + 16 * MAXN;
+static_assert(OFF_ZE + 16 * MAXN <= PSZ, "prep scratch must fit in P");
+
+struct SharedC1 {
+  float P[PSZ];
+  float BdtT[12][16];
+  float ibuf[NV];          // 1 / sqrt(d_k) of pivot k
+  float gbuf[NV];          // gradient border of pivot k
+  float vbuf[NV];          // broadcast vector (y, then masked d)
+  float bufA[NV], bufB[NV];  // published J rows ia, iz
+  float xs[NV];
+  float cs[2 * NV];        // Givens (c, s) per column pair
+  float sub[4 * MAXN];     // ub of each stance foot-step (gait * f_max)
+  int sfs[4 * MAXN];       // stance foot-step ids, in order
+  int blkbase[MAXN + 2];   // first reduced variable of each horizon step
+  unsigned char varblk[NV], varcol[NV];
+  unsigned char stance[4 * MAXN];
+  unsigned char cflag[2 * NV + 8];  // active flag per constraint id (6 per stance foot-step)
+};
+
+__device__ __forceinline__ void lsync() {
+  // single-wavefront workgroup: LDS ops of one wave execute in issue order; this only stops
+  // the compiler from moving LDS accesses across the point
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ float fdiv(float a, float b) { return a * fast_rcp(b); }
+
+// Register pin: forces every row element to be materialised at this point. Without it LLVM sinks
+// the right-looking updates of slot[c] down to the step that first reads slot[c] (turning the
+// factorisation left-looking in registers: O(n) multipliers and pivot values live per column,
+// >1000 VGPR spills).
+template <int M>
+__device__ __forceinline__ void pin(float (&x)[M]) {
+#pragma unroll
+  for (int c = 0; c < M; c++) asm volatile("" : "+v"(x[c]));
+}
+
+// Scheduling fence inside long unrolled LDS->FMA sweeps: without it the scheduler issues every
+// ds_read_b128 of a row up front (64 extra live VGPRs on top of the 65-slot row).
+#define CMPC_SWEEP_FENCE(c)                                  \
+  do {                                                       \
+    if (((c) & 15) == 12) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
+__device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KParams& P,
+                                         SharedC1& sh, float* __restrict__ fout,
+                                         uint8_t* __restrict__ st_out, int32_t* __restrict__ it_out,
+                                         int* __restrict__ ovf_list, int* __restrict__ ovf_count,
+                                         int inst) {
+  const int v = threadIdx.x;
+  const int N = P.N;
+  // ---- stance table + elimination: eliminated iff |gait * f_max| < 0.01 (SolverMPC.cpp:869-894)
+  const unsigned char* gait = reinterpret_cast<const unsigned char*>(rec + CMPC_REC_HDR + 12 * N);
+  int nfs = 0;
+  for (int c0 = 0; c0 < 4 * N; c0 += 64) {
+    const int t = c0 + v;
+    float ub = 0.f;
+    bool f = false;
+    if (t < 4 * N) {
+      ub = (float)gait[t] * P.f_max;
+      f = !(ub < 0.01f && ub > -0.01f);
+      sh.stance[t] = f ? 1 : 0;
+    }
+    const unsigned long long m = __ballot(f);
+    const int pre = __popcll(m & ((1ull << v) - 1ull));
+    if (f) {
+      sh.sfs[nfs + pre] = t;
+      sh.sub[nfs + pre] = ub;
+    }
+    nfs += __popcll(m);
+  }
+  const int n = 3 * nfs;
+  if (n > NV) {  // hand the instance to the next size class
+    if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
+    return;
+  }
+  lsync();
+  {
+    int kb = 0, kc = 0;
+    if (v < n) {
+      const int fs = sh.sfs[v / 3];
+      kb = fs >> 2;
+      kc = 3 * (fs & 3) + v % 3;
+    }
+    sh.varblk[v] = (unsigned char)kb;
+    sh.varcol[v] = (unsigned char)kc;
+    if (v <= N) {
+      int c = 0;
+      for (int s = 0; s < nfs; s++) c += (sh.sfs[s] < 4 * v) ? 1 : 0;
+      sh.blkbase[v] = 3 * c;
+    }
+    for (int t = v; t < 6 * nfs; t += 64) sh.cflag[t] = 0;
+    for (int t = v; t < 12 * N; t += 64) sh.P[OFF_TRAJ + t] = rec[CMPC_REC_HDR + t];
+  }
+  Model md;
+  make_model(rec, P.dt, md);
+  make_bdt<64>(rec, md, v, sh.BdtT);
+  lsync();
+  if (v < N) {
+    float e[13];
+    state_error(rec, md, v, &sh.P[OFF_TRAJ + 12 * v], e);
+#pragma unroll
+    for (int j = 0; j < 13; j++) sh.P[OFF_E + 16 * v + j] = e[j];
+  }
+  lsync();
+  float wts[13];
+#pragma unroll
+  for (int j = 0; j < 12; j++) wts[j] = P.wts[j];
+  wts[12] = 0.f;
+  // gradient recursion ze_i = S e_i + Adt' ze_{i+1} (uniform: every lane computes it, lane j
+  // stores component j)
+  {
+    float ze[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) ze[j] = 0.f;
+    for (int i = N - 1; i >= 0; i--) {
+      float e[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) e[j] = sh.P[OFF_E + 16 * i + j];
+      recur(md, wts, e, ze);
+      float mine = 0.f;
+#pragma unroll
+      for (int j = 0; j < 13; j++) mine = (v == j) ? ze[j] : mine;
+      if (v < 13) sh.P[OFF_ZE + 16 * i + v] = mine;
+    }
+  }
+  lsync();
+
+  // ---- condensation: lane v builds H[v][w] for w >= v into packed P, and its gradient g_v
+  const bool real = v < n;
+  float gv;
+  {
+    const int kv = real ? sh.varblk[v] : 0;
+    const int cv = real ? sh.varcol[v] : 0;
+    float b[13], u1[13], u2[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) b[j] = real ? sh.BdtT[cv][j] : 0.f;
+    n1_mul(md, b, u1);
+    n1_mul(md, u1, u2);
+    {
+      float zk[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) zk[j] = sh.P[OFF_ZE + 16 * kv + j];
+      gv = real ? 2.f * dot13(b, zk) : 0.f;  // qg = 2 B_qp' S (A_qp x0 + Q_qp f - X_d)
+    }
+    lsync();  // every ZE read is issued before P is overwritten
+    const int myrow = prow0(v);
+    float z[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) z[j] = 0.f;
+    for (int i = N - 1; i >= 0; i--) {
+      // z_i = S Adt^{i-kv} b_v + Adt' z_{i+1}  (the S term only for i >= kv)
+      const bool act = real && (i >= kv);
+      const float k = (float)(i - kv);
+      const float k2 = 0.5f * k * (k - 1.f);
+      float gk[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) gk[j] = act ? fmaf(k2, u2[j], fmaf(k, u1[j], b[j])) : 0.f;
+      recur(md, wts, gk, z);
+      const int wb = __builtin_amdgcn_readfirstlane(sh.blkbase[i]);
+      const int we = __builtin_amdgcn_readfirstlane(sh.blkbase[i + 1]);
+      for (int w = wb; w < we; w++) {
+        const int cw = sh.varcol[w];
+        float bw[13];
+#pragma unroll
+        for (int j = 0; j < 13; j++) bw[j] = sh.BdtT[cw][j];
+        float val = 2.f * dot13(bw, z);
+        if (w == v) val += P.alpha2;  // qH = 2 (B'SB + alpha I), SolverMPC.cpp:806
+        if (act && w >= v) sh.P[myrow + w] = val;
+      }
+    }
+  }
+  lsync();
+
+  // ---- row v of H into registers (full symmetric; identity padding for v >= n) ----------
+  float slot[NV + 1];
+  {
+    const int myrow = prow0(v);
+    static_for<0, NV>([&](auto C) {
+      constexpr int c = decltype(C)::value;
+      const int addr = (c >= v) ? myrow + c : prow0(c) + v;
+      const float x = sh.P[addr];
+      slot[c] = (real && c < n) ? x : ((c == v) ? 1.f : 0.f);
+      if ((c & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    });
+    slot[NV] = gv;
+  }
+  lsync();
+
+  // ---- bordered Cholesky [H | g]: raw column k = slot[k] of every lane -> P row k ----------
+  int status = CMPC_OK;
+  float my_inv = 1.f;
+  static_for<0, NV>([&](auto KC) {
+    constexpr int k = decltype(KC)::value;
+    constexpr int c0 = k & ~3;
+    constexpr int rk = prow(k);
+    if (k < n) {
+      if (v >= c0) sh.P[rk + v - c0] = (v >= k) ? slot[k] : 0.f;
+      if (v == k) sh.gbuf[k] = slot[NV];
+      lsync();
+      float d = sh.P[rk + k - c0];
+      if (!(d > 0.f)) { status = CMPC_NOT_PD; d = 1e-30f; }
+      const float inv = rsqrtf(d);
+      if (v == k) { my_inv = inv; sh.ibuf[k] = inv; }
+      const float a = (v > k) ? -slot[k] * (inv * inv) : 0.f;
+#pragma unroll
+      for (int c = c0; c < NV; c += 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
+        slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
+        slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
+        slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
+        slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+        CMPC_SWEEP_FENCE(c);
+      }
+      slot[NV] = fmaf(a, sh.gbuf[k], slot[NV]);
+      pin(slot);
+    }
+  });
+  const float yv = (v < n) ? slot[NV] * my_inv : 0.f;  // L y = g
+  lsync();
+
+  // ---- J = L^-T: lane v solves L x = e_v (column v of L^-1 = row v of J) -----------------
+  static_for<0, NV>([&](auto C) {
+    constexpr int c = decltype(C)::value;
+    slot[c] = (c == v) ? 1.f : 0.f;
+  });
+  static_for<0, NV>([&](auto KC) {
+    constexpr int k = decltype(KC)::value;
+    constexpr int c0 = k & ~3;
+    constexpr int rk = prow(k);
+    if (k < n) {
+      lsync();
+      const float inv = sh.ibuf[k];
+      const float xk = slot[k] * inv;
+      const float a = -xk * inv;
+#pragma unroll
+      for (int c = c0; c < NV; c += 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
+        slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
+        slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
+        slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
+        slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+        CMPC_SWEEP_FENCE(c);
+      }
+      slot[k] = xk;
+      pin(slot);
+    }
+  });
+
+  // ---- unconstrained minimiser x = -J y ----------------------------------------------------
+  sh.vbuf[v] = yv;
+  lsync();
+  float xv = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; c += 4) {
+    const float4 y4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+    xv = fmaf(slot[c + 0], y4.x, xv);
+    xv = fmaf(slot[c + 1], y4.y, xv);
+    xv = fmaf(slot[c + 2], y4.z, xv);
+    xv = fmaf(slot[c + 3], y4.w, xv);
+    CMPC_SWEEP_FENCE(c);
+  }
+  xv = (v < n) ? -xv : 0.f;
+  lsync();
+
+  // ---- Goldfarb-Idnani dual active set on the friction pyramids -----------------------------
+  const float mui = P.mu_inv;
+  const float fnorm = rsqrtf(mui * mui + 1.f);
+  int q = 0;
+  int iters = 0;
+  float u_reg = 0.f;   // lane j < q: dual of active constraint j
+  int act_reg = 0;     // lane j < q: id of active constraint j
+  if (status == CMPC_OK) {
+    for (;;) {
+      sh.xs[v] = xv;
+      lsync();
+      float best = 0.f;
+      int bid = 0x7fffffff;
+      if (v < nfs) {
+        const float fx = sh.xs[3 * v], fy = sh.xs[3 * v + 1], fz = sh.xs[3 * v + 2];
+        float sl[6];
+        sl[0] = (mui * fx + fz) * fnorm;
+        sl[1] = (-mui * fx + fz) * fnorm;
+        sl[2] = (mui * fy + fz) * fnorm;
+        sl[3] = (-mui * fy + fz) * fnorm;
+        sl[4] = fz;
+        sl[5] = sh.sub[v] - fz;
+#pragma unroll
+        for (int t = 0; t < 6; t++)
+          if (!sh.cflag[6 * v + t] && sl[t] < best) { best = sl[t]; bid = 6 * v + t; }
+      }
+      const float xmax = wave_max(fabsf(xv));
+      wave_argmin(best, bid);
+      const float tol = 1e-5f * fmaxf(1.f, xmax);
+      if (bid == 0x7fffffff || best >= -tol) break;
+
+      const int p = __builtin_amdgcn_readfirstlane(bid);
+      const Cons cp = decode_cons(p, mui, sh.sub[p / 6]);
+      float up = 0.f;
+      for (;;) {
+        if (++iters > P.max_iter) { status = CMPC_MAX_ITER; break; }
+        pin(slot);
+        // d = J' n+ : rows ia, iz of J through LDS
+        if (v == cp.ia && cp.ia != cp.iz) {
+#pragma unroll
+          for (int c = 0; c < NV; c += 4)
+            *reinterpret_cast<float4*>(&sh.bufA[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
+        }
+        if (v == cp.iz) {
+#pragma unroll
+          for (int c = 0; c < NV; c += 4)
+            *reinterpret_cast<float4*>(&sh.bufB[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
+        }
+        lsync();
+        const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[v], cp.cb * sh.bufB[v]) : cp.cb * sh.bufB[v];
+        sh.vbuf[v] = (v >= q) ? dv : 0.f;
+        lsync();
+        // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+, dn = |d|^2
+        float zv = 0.f;
+#pragma unroll
+        for (int c = 0; c < NV; c += 4) {
+          const float4 m4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+          zv = fmaf(slot[c + 0], m4.x, zv);
+          zv = fmaf(slot[c + 1], m4.y, zv);
+          zv = fmaf(slot[c + 2], m4.z, zv);
+          zv = fmaf(slot[c + 3], m4.w, zv);
+          CMPC_SWEEP_FENCE(c);
+        }
+        const float dsq = (v < n) ? dv * dv : 0.f;
+        const float dn = wave_sum(dsq);
+        const float zn = wave_sum((v >= q) ? dsq : 0.f);
+        // r = R^-1 d1, R[i][j] = J[:,i]' n_j: back substitution through m = sum_{j>i} r_j n_j
+        float m = 0.f, r_reg = 0.f;
+        static_for<0, NV>([&](auto IC) {
+          constexpr int i = NV - 1 - decltype(IC)::value;
+          if (i < q) {
+            const int ai = rli(act_reg, i);
+            const Cons ci = decode_cons(ai, mui, sh.sub[ai / 6]);
+            const float ja = rl(slot[i], ci.ia), jz = rl(slot[i], ci.iz);
+            const float Rii = fmaf(ci.ca, ja, ci.cb * jz);
+            const float sdot = wave_sum(slot[i] * m);
+            const float ri = fdiv(rl(dv, i) - sdot, Rii);
+            r_reg = (v == i) ? ri : r_reg;
+            if (v == ci.ia) m = fmaf(ci.ca, ri, m);
+            if (v == ci.iz) m = fmaf(ci.cb, ri, m);
+          }
+        });
+        // partial (dual) step t1, full (primal) step t2
+        float t1 = kBigF;
+        int kk = 0x7fffffff;
+        if (v < q && r_reg > 0.f) { t1 = fmaxf(fdiv(u_reg, r_reg), 0.f); kk = v; }
+        wave_argmin(t1, kk);
+        const float spv = fmaf(cp.ca, rl(xv, cp.ia), fmaf(cp.cb, rl(xv, cp.iz), -cp.bp));
+        const bool zero_step = !(zn > 1e-9f * dn);
+        const float t2 = zero_step ? kBigF : -fdiv(spv, zn);
+        const float t = fminf(t1, t2);
+        if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
+        if (v < q) u_reg = fmaf(-t, r_reg, u_reg);
+        up += t;
+        if (!zero_step) xv = fmaf(t, zv, xv);
+        if (!zero_step && t2 <= t1) {
+          // ---- add p: Givens rotations zeroing d[q+1..n-1] into d[q]; parameters in closed
+          // form from suffix norms ts_j = |d[j..n-1]|
+          const float ts = sqrtf(wave_suffix_sum((v >= q && v < n) ? dv * dv : 0.f, v));
+          const float ts_prev = __shfl_up(ts, 1, 64);
+          const float d_prev = __shfl_up(dv, 1, 64);
+          float cj = 1.f, sj = 0.f;
+          if (v > q && v < n && ts_prev > 0.f) {
+            const float ri = fast_rcp(ts_prev);
+            cj = d_prev * ri;
+            sj = ((v == n - 1) ? dv : ts) * ri;
+          }
+          *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(cj, sj);
+          lsync();
+          static_for<0, NV - 1>([&](auto IC) {
+            constexpr int j = NV - 1 - decltype(IC)::value;  // NV-1 .. 1
+            if ((unsigned)(j - q - 1) < (unsigned)(n - q - 1)) {  // q < j < n
+              const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+              const float a0 = slot[j - 1], b0 = slot[j];
+              slot[j - 1] = fmaf(cs2.x, a0, cs2.y * b0);
+              slot[j] = fmaf(-cs2.y, a0, cs2.x * b0);
+            }
+          });
+          pin(slot);
+          if (v == q) { u_reg = up; act_reg = p; }
+          if (v == 0) sh.cflag[p] = 1;
+          q++;
+          lsync();
+          break;
+        }
+        // ---- drop active constraint kk, re-triangularise the implicit R -------------------
+        {
+          const int k = __builtin_amdgcn_readfirstlane(kk);
+          const int ak = rli(act_reg, k);
+          if (v == 0) sh.cflag[ak] = 0;
+          const int a_nx = __shfl_down(act_reg, 1, 64);
+          const float u_nx = __shfl_down(u_reg, 1, 64);
+          if (v >= k && v < q - 1) { act_reg = a_nx; u_reg = u_nx; }
+          static_for<0, NV - 1>([&](auto JC) {
+            constexpr int j = decltype(JC)::value;  // 0 .. NV-2
+            if ((unsigned)(j - k) < (unsigned)(q - 1 - k)) {  // k <= j < q-1
+              const int aj = rli(act_reg, j);
+              const Cons c2 = decode_cons(aj, mui, sh.sub[aj / 6]);
+              const float a0 = fmaf(c2.ca, rl(slot[j], c2.ia), c2.cb * rl(slot[j], c2.iz));
+              const float b0 = fmaf(c2.ca, rl(slot[j + 1], c2.ia), c2.cb * rl(slot[j + 1], c2.iz));
+              const float h = sqrtf(a0 * a0 + b0 * b0);
+              float c = 1.f, sn = 0.f;
+              if (h > 0.f) { const float ih = fast_rcp(h); c = a0 * ih; sn = b0 * ih; }
+              const float x0 = slot[j], x1 = slot[j + 1];
+              slot[j] = fmaf(c, x0, sn * x1);
+              slot[j + 1] = fmaf(-sn, x0, c * x1);
+            }
+          });
+          pin(slot);
+          q--;
+          lsync();
+        }
+      }
+      if (status != CMPC_OK) break;
+    }
+  }
+
+  // ---- scatter (q_soln layout 12 k + 3 leg + axis, swing -> 0) staged in LDS, coalesced out
+  const bool ok = (status == CMPC_OK);
+  for (int t = v; t < 12 * N; t += 64) sh.P[t] = 0.f;
+  lsync();
+  if (ok && v < n) sh.P[12 * sh.varblk[v] + sh.varcol[v]] = xv;
+  lsync();
+  for (int t = 4 * v; t < 12 * N; t += 256)
+    *reinterpret_cast<float4*>(&fout[t]) = *reinterpret_cast<const float4*>(&sh.P[t]);
+  if (v == 0) {
+    st_out[0] = (uint8_t)status;
+    if (it_out) it_out[0] = iters;
   }
 }
 
+}  // namespace
+
+__global__ __launch_bounds__(64, CMPC_W1_WAVES_PER_EU) void cmpc_solve_c1_kernel(
+    const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
+    uint8_t* __restrict__ status, int32_t* __restrict__ iters, int* __restrict__ ovf_list,
+    int* __restrict__ ovf_count) {
+  // one instance per workgroup, no grid-stride loop: a loop around the solve would let LICM
+  // hoist hundreds of lane-invariant addresses / masks out of it and spill them
+  __shared__ SharedC1 sh;
+  const int t = blockIdx.x;
+  if (t >= batch) return;
+  solve_c1(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * 12 * P.N, status + t,
+           iters ? iters + t : nullptr, ovf_list, ovf_count, t);
+}
+
 hipError_t launch_class1(const float* d_recs, int batch, const KParams& P, float* d_forces,
-                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
-                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(cmpc_solve_reg_kernel<1>, dim3(grid), dim3(64), 0, stream, d_recs, batch, P,
-                     d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
+                         uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
+                         int* ovf_list, int* ovf_count, int grid, hipStream_t stream) {
+  (void)in_list;
+  (void)in_count;
+  hipLaunchKernelGGL(cmpc_solve_c1_kernel, dim3(grid), dim3(64), 0, stream, d_recs, batch, P,
+                     d_forces, d_status, d_iters, ovf_list, ovf_count);
   return hipGetLastError();
 }
 

@@ -1,0 +1,281 @@
+#pragma once
+// cmpc_common.h — device building blocks shared by every solver kernel:
+//   * wavefront reductions / lane helpers (64-wide wavefronts, gfx950);
+//   * the per-instance model of solve_mpc(): RobotState::set + quat_to_rpy
+//     (RobotState.cpp:9-50, SolverMPC.cpp:352-361), ct_ss_mats (SolverMPC.cpp:260-279) and the
+//     closed-form discretisation of c2qp (SolverMPC.cpp:96-107; A_c^3 = 0 so
+//     expm(dt [A B Q; 0]) = I + M + M^2/2 + M^3/6 exactly);
+//   * the stance table / swing elimination (SolverMPC.cpp:859-894) and the condensation
+//     recursions that build the reduced qH / qg (SolverMPC.cpp:806-814) without ever forming
+//     A_qp, B_qp or the dense 13N x 13N weight matrix S.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "cmpc_kernels.h"
+
+namespace cmpc {
+namespace {
+
+constexpr int MAXN = CMPC_MAX_HORIZON;
+constexpr float kBigF = 3.0e38f;
+
+// ---------------------------------------------------------------------------------------------
+// wavefront helpers
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+// argmin with a deterministic tie-break on the smaller index
+__device__ __forceinline__ void wave_argmin(float& v, int& i) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float ov = __shfl_xor(v, off, 64);
+    const int oi = __shfl_xor(i, off, 64);
+    if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+}
+// inclusive suffix sum over lanes: s_l = sum_{m >= l} v_m
+__device__ __forceinline__ float wave_suffix_sum(float v, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float t = __shfl_down(v, off, 64);
+    if (lane + off < 64) v += t;
+  }
+  return v;
+}
+
+template <int I, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < E) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, E>(f);
+  }
+}
+
+__device__ __forceinline__ float rl(float x, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
+}
+__device__ __forceinline__ int rli(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
+// An SGPR value the compiler cannot see through: keeps per-iteration scalar work of an unrolled
+// loop inside its iteration (otherwise LICM hoists dozens of SGPRs out of it -> spills).
+__device__ __forceinline__ int opaque(int x) {
+  x = __builtin_amdgcn_readfirstlane(x);
+  asm volatile("" : "+s"(x));
+  return x;
+}
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// single-wavefront workgroup: orders this wave's LDS traffic without an s_barrier
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Discretised model (closed form). Adt = I + N1 with N1 = dt A_c + dt^2/2 A_c^2 (16 structural
+// nonzeros); Adt^m = I + m N1 + m(m-1)/2 N1^2 exactly (N1^3 = 0).
+// ---------------------------------------------------------------------------------------------
+struct Model {
+  float R[9];      // body rotation (Eigen toRotationMatrix of q, w-first); R_yaw = R (RobotState.cpp:44)
+  float n1r[9];    // N1[0..2][6..8] = dt * R^T
+  float dt, dth, xdrag;  // dt, dt^2/2, x_drag (A_c(11,9), SolverMPC.cpp:277)
+};
+
+// y = N1 x   (13-vectors)
+__device__ __forceinline__ void n1_mul(const Model& m, const float* x, float* y) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) y[i] = m.n1r[i * 3 + 0] * x[6] + m.n1r[i * 3 + 1] * x[7] + m.n1r[i * 3 + 2] * x[8];
+  y[3] = m.dt * x[9];
+  y[4] = m.dt * x[10];
+  y[5] = m.dt * x[11] + (m.dth * m.xdrag) * x[9] + m.dth * x[12];
+#pragma unroll
+  for (int i = 6; i < 11; i++) y[i] = 0.f;
+  y[11] = (m.dt * m.xdrag) * x[9] + m.dt * x[12];
+  y[12] = 0.f;
+}
+
+// z <- w .* e + Adt' z   (in place on z; Adt' = I + N1')
+__device__ __forceinline__ void recur(const Model& m, const float* wts, const float* e, float* z) {
+  float t[13];
+#pragma unroll
+  for (int j = 0; j < 13; j++) t[j] = z[j];
+  const float c6 = m.n1r[0] * t[0] + m.n1r[3] * t[1] + m.n1r[6] * t[2];
+  const float c7 = m.n1r[1] * t[0] + m.n1r[4] * t[1] + m.n1r[7] * t[2];
+  const float c8 = m.n1r[2] * t[0] + m.n1r[5] * t[1] + m.n1r[8] * t[2];
+  const float c9 = m.dt * t[3] + (m.dt * m.xdrag) * t[11] + (m.dth * m.xdrag) * t[5];
+  const float c10 = m.dt * t[4];
+  const float c11 = m.dt * t[5];
+  const float c12 = m.dt * t[11] + m.dth * t[5];
+#pragma unroll
+  for (int j = 0; j < 13; j++) z[j] = wts[j] * e[j] + t[j];
+  z[6] += c6; z[7] += c7; z[8] += c8; z[9] += c9; z[10] += c10; z[11] += c11; z[12] += c12;
+}
+
+__device__ __forceinline__ float dot13(const float* a, const float* b) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 13; j++) s = fmaf(a[j], b[j], s);
+  return s;
+}
+
+// quaternion (w,x,y,z) -> rotation matrix, as Eigen's toRotationMatrix (RobotState.cpp:36)
+__device__ __forceinline__ void make_model(const float* __restrict__ rec, float dt, Model& md) {
+  const float qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],
+              qz = rec[CMPC_REC_Q + 3];
+  const float tx = 2.f * qx, ty = 2.f * qy, tz = 2.f * qz;
+  const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+  const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+  const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+  md.R[0] = 1.f - (tyy + tzz); md.R[1] = txy - twz;         md.R[2] = txz + twy;
+  md.R[3] = txy + twz;         md.R[4] = 1.f - (txx + tzz); md.R[5] = tyz - twx;
+  md.R[6] = txz - twy;         md.R[7] = tyz + twx;         md.R[8] = 1.f - (txx + tyy);
+  md.dt = dt;
+  md.dth = dt * dt * 0.5f;
+  md.xdrag = rec[CMPC_REC_XDRAG];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) md.n1r[i * 3 + j] = dt * md.R[j * 3 + i];
+}
+
+// Bdt[s][c] for thread-strided entries t = s + 13 c (c = 3 leg + axis) -> BdtT[c][s]
+// (ct_ss_mats B_c rows 6..11: I_world^-1 [r]x, I/m; SolverMPC.cpp:267-276, m = 12 RobotState.h:26,
+// I_body = diag(.07, .26, .242) RobotState.h:25; I_world = R I_body R^T, SolverMPC.cpp:593)
+template <int NT>
+__device__ __forceinline__ void make_bdt(const float* __restrict__ rec, const Model& md, int tid,
+                                         float (*BdtT)[16]) {
+  const float Ib[3] = {.07f, 0.26f, 0.242f};
+  float Iw[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      Iw[i * 3 + j] = md.R[i * 3 + 0] * Ib[0] * md.R[j * 3 + 0] + md.R[i * 3 + 1] * Ib[1] * md.R[j * 3 + 1] +
+                      md.R[i * 3 + 2] * Ib[2] * md.R[j * 3 + 2];
+  const float c00 = Iw[4] * Iw[8] - Iw[5] * Iw[7];
+  const float c10 = Iw[5] * Iw[6] - Iw[3] * Iw[8];
+  const float c20 = Iw[3] * Iw[7] - Iw[4] * Iw[6];
+  const float idet = 1.f / (Iw[0] * c00 + Iw[1] * c10 + Iw[2] * c20);
+  float Ii[9];
+  Ii[0] = c00 * idet; Ii[1] = (Iw[2] * Iw[7] - Iw[1] * Iw[8]) * idet; Ii[2] = (Iw[1] * Iw[5] - Iw[2] * Iw[4]) * idet;
+  Ii[3] = c10 * idet; Ii[4] = (Iw[0] * Iw[8] - Iw[2] * Iw[6]) * idet; Ii[5] = (Iw[2] * Iw[3] - Iw[0] * Iw[5]) * idet;
+  Ii[6] = c20 * idet; Ii[7] = (Iw[1] * Iw[6] - Iw[0] * Iw[7]) * idet; Ii[8] = (Iw[0] * Iw[4] - Iw[1] * Iw[3]) * idet;
+  const float im = 1.f / 12.0f;
+  const float dt = md.dt, dt2 = md.dth, dt3 = md.dt * md.dt * md.dt / 6.f;
+  for (int t = tid; t < 13 * 12; t += NT) {
+    const int s = t % 13, c = t / 13;
+    const int b = c / 3, a = c % 3;
+    const float r0 = rec[CMPC_REC_R + 0 * 4 + b], r1 = rec[CMPC_REC_R + 1 * 4 + b], r2 = rec[CMPC_REC_R + 2 * 4 + b];
+    float cx[3];  // column a of [r]x
+    if (a == 0) { cx[0] = 0.f; cx[1] = r2; cx[2] = -r1; }
+    else if (a == 1) { cx[0] = -r2; cx[1] = 0.f; cx[2] = r0; }
+    else { cx[0] = r1; cx[1] = -r0; cx[2] = 0.f; }
+    float T[3];  // B_c[6+i][c] = (I_inv [r]x)[i][a]
+#pragma unroll
+    for (int i = 0; i < 3; i++) T[i] = Ii[i * 3 + 0] * cx[0] + Ii[i * 3 + 1] * cx[1] + Ii[i * 3 + 2] * cx[2];
+    const float b9 = (a == 0) ? im : 0.f;  // B_c[9][c]
+    float val = 0.f;
+    if (s < 3) {
+      const float c0 = (s == 0) ? md.R[0] : (s == 1) ? md.R[1] : md.R[2];
+      const float c1 = (s == 0) ? md.R[3] : (s == 1) ? md.R[4] : md.R[5];
+      const float c2 = (s == 0) ? md.R[6] : (s == 1) ? md.R[7] : md.R[8];
+      val = dt2 * (c0 * T[0] + c1 * T[1] + c2 * T[2]);
+    } else if (s < 6) {
+      val = dt2 * (((s - 3) == a) ? im : 0.f);
+      if (s == 5) val += dt3 * md.xdrag * b9;
+    } else if (s < 9) {
+      val = dt * ((s == 6) ? T[0] : (s == 7) ? T[1] : T[2]);
+    } else if (s < 12) {
+      val = dt * (((s - 9) == a) ? im : 0.f);
+      if (s == 11) val += dt2 * md.xdrag * b9;
+    }
+    BdtT[c][s] = val;
+  }
+  for (int t = tid; t < 12 * 3; t += NT) BdtT[t / 3][13 + t % 3] = 0.f;
+}
+
+// e_i = Adt^{i+1} x0 + sum_{k<=i} Adt^k Qdt f - X_d,i for step i (SolverMPC.cpp:592, 633-642,
+// 808-814). x0 = [rpy, p, w, v, -9.8] with rpy from quat_to_rpy (SolverMPC.cpp:352-361).
+__device__ __forceinline__ void state_error(const float* __restrict__ rec, const Model& md, int i,
+                                            const float* traj_i, float* e) {
+  const float qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],
+              qz = rec[CMPC_REC_Q + 3];
+  float x0[13];
+  {
+    float as = -2.f * (qx * qz - qw * qy);
+    as = fminf(as, 0.99999f);  // only the upper clamp, as the reference
+    x0[0] = atan2f(2.f * (qy * qz + qw * qx), qw * qw - qx * qx - qy * qy + qz * qz);
+    x0[1] = asinf(as);
+    x0[2] = atan2f(2.f * (qx * qy + qw * qz), qw * qw + qx * qx - qy * qy - qz * qz);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      x0[3 + k] = rec[CMPC_REC_P + k];
+      x0[6 + k] = rec[CMPC_REC_W + k];
+      x0[9 + k] = rec[CMPC_REC_V + k];
+    }
+    x0[12] = -9.8f;
+  }
+  float X1[13], X2[13], qf[13], F1[13], F2[13];
+  n1_mul(md, x0, X1);
+  n1_mul(md, X1, X2);
+  // Q_qp f with f = (0,0,0,f_est(3),0,0) when the history flag is set (SolverMPC.cpp:808-811)
+  const uint32_t flags = __float_as_uint(rec[CMPC_REC_FLAGS]);
+  const float f3 = (flags & 1u) ? rec[CMPC_REC_FEST3] : 0.f;
+#pragma unroll
+  for (int j = 0; j < 13; j++) qf[j] = 0.f;
+  // Qdt[:,3] = dt e9 + dt^2/2 (e3 + xdrag e11) + dt^3/6 xdrag e5
+  qf[9] = md.dt * f3;
+  qf[3] = md.dth * f3;
+  qf[11] = md.dth * md.xdrag * f3;
+  qf[5] = (md.dt * md.dt * md.dt / 6.f) * md.xdrag * f3;
+  n1_mul(md, qf, F1);
+  n1_mul(md, F1, F2);
+  const float m1 = (float)(i + 1);
+  const float m2 = 0.5f * m1 * (float)i;
+  const float s2 = 0.5f * (float)i * (float)(i + 1);
+  const float s3 = (float)(i + 1) * (float)i * (float)(i - 1) / 6.f;
+#pragma unroll
+  for (int j = 0; j < 13; j++) {
+    float ev = x0[j] + m1 * X1[j] + m2 * X2[j] + m1 * qf[j] + s2 * F1[j] + s3 * F2[j];
+    if (j < 12) ev -= traj_i[j];
+    e[j] = ev;
+  }
+}
+
+// Friction-pyramid constraint c = 6 s + t of stance foot-step s (reduced vars 3s, 3s+1, 3s+2):
+//   t = 0..3: +-fx/mu + fz >= 0, +-fy/mu + fz >= 0 ; t = 4: fz >= 0 ; t = 5: -fz >= -ub
+// (fmat rows of SolverMPC.cpp:657-665 with lb = 0, ub = BIG / gait*f_max)
+struct Cons {
+  int ia, iz;
+  float ca, cb, bp;
+};
+__device__ __forceinline__ Cons decode_cons(int c, float mui, float sub_s) {
+  Cons k;
+  const int sft = c / 6, t = c - 6 * (c / 6);
+  k.iz = 3 * sft + 2;
+  if (t < 4) {
+    k.ia = 3 * sft + (t >> 1);
+    k.ca = (t & 1) ? -mui : mui;
+    k.cb = 1.f;
+    k.bp = 0.f;
+  } else {
+    k.ia = k.iz;
+    k.ca = 0.f;
+    k.cb = (t == 4) ? 1.f : -1.f;
+    k.bp = (t == 4) ? 0.f : -sub_s;
+  }
+  return k;
+}
+
+}  // namespace
+}  // namespace cmpc

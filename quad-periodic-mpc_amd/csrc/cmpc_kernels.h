@@ -22,20 +22,27 @@ struct KParams {
 
 // Scratch ints needed by launch_solve for max_batch instances.
 inline size_t work_ints(int max_batch) { return 4 + 2 * (size_t)max_batch; }
+// Workgroups of the general class (persistent over its overflow list) and its global slabs.
+inline int classg_grid(int max_batch) { return max_batch < 512 ? max_batch : 512; }
+size_t classg_scratch_floats(int horizon, int grid);
 
-// ev (optional): 3 events recorded around the two size-class launches
-// (ev[0] before class 1, ev[1] between, ev[2] after class 2).
+// ev (optional): 3 events recorded around the size-class launches
+// (ev[0] before class 1, ev[1] between class 1 and the wider classes, ev[2] after them).
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
-                        hipStream_t stream, hipEvent_t* ev = nullptr);
-// per-class launchers (cmpc_class1.hip, cmpc_class2.hip)
+                        float* d_gscratch, hipStream_t stream, hipEvent_t* ev = nullptr);
+// per-class launchers (cmpc_class1.hip, cmpc_class2.hip, cmpc_classg.hip)
 hipError_t launch_class1(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
 hipError_t launch_class2(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
+hipError_t launch_classg(const float* d_recs, int batch, const KParams& P, float* d_forces,
+                         uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
+                         float* scratch, int grid, hipStream_t stream);
+// parity hook: full (nothing eliminated) qH [12N x 12N] / qg [12N] per instance
 hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
-                           hipStream_t stream);
+                           float* scratch, int grid, hipStream_t stream);
 
 }  // namespace cmpc

@@ -14,6 +14,6 @@ for name in GOLDEN_SETS:
     f, st, it = s.solve_host(g["records"])
     e = rel_force_err(f, g["q_ref"]).max()
     worst = max(worst, e)
-    print(f"{name:12s} status={np.bincount(st, minlength=5).tolist()} max_rel_err={e:.2e} iters={it.mean():.1f}")
+    print(f"{name:14s} status={np.bincount(st, minlength=5).tolist()} max_rel_err={e:.2e} iters={it.mean():.1f}")
 print("WORST", worst)
 sys.exit(0 if worst <= 2e-4 else 3)

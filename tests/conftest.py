@@ -39,7 +39,8 @@ def golden_params(cm, g):
                           alpha=float(g["alpha"]))
 
 
-GOLDEN_SETS = ["n10_mixed", "n10_stress", "n10_edge", "n16_trot", "n19_mixed", "n20_trot"]
+GOLDEN_SETS = ["n10_mixed", "n10_stress", "n10_edge", "n16_trot", "n19_mixed", "n20_trot",
+               "n20_mixed", "n12_allstance"]
 
 
 def rel_force_err(f, f_ref):

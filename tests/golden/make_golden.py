@@ -39,6 +39,15 @@ def edge_records(N: int) -> np.ndarray:
     return recs
 
 
+def allstance_records(N: int, count: int) -> np.ndarray:
+    """Every leg in stance at every step: n = 12 N (the largest reduced QP of a horizon)."""
+    recs = cm.make_instances(count, N, seed=1007, random_contact_frac=0.0)
+    off = cm.records.gait_offset(N)
+    ones = np.ones((count, 4 * N), np.uint8)
+    recs[:, off:off + N] = ones.view(np.float32).reshape(count, N)
+    return recs
+
+
 def build_set(name, records, prm, cond_count=0):
     q, st, nw = orc.ref_solve_batch(records, prm, nthreads=8)
     out = dict(records=records, horizon=prm.horizon, dt=prm.dt, mu=prm.mu, f_max=prm.f_max,
@@ -65,6 +74,10 @@ def main():
     build_set("n19_mixed", cm.make_instances(8, 19, seed=1004), cm.make_params(19))
     build_set("n20_trot", cm.make_instances(8, 20, seed=1005, random_contact_frac=0.0),
               cm.make_params(20), cond_count=1)
+    # general size class (n > 128): random contacts at N = 20 and all-stance at N = 12
+    build_set("n20_mixed", cm.make_instances(16, 20, seed=1006, random_contact_frac=1.0),
+              cm.make_params(20))
+    build_set("n12_allstance", allstance_records(12, 4), cm.make_params(12), cond_count=1)
 
 
 if __name__ == "__main__":

@@ -77,7 +77,8 @@ def test_edge_cases(cm, solver_mod):
 
 
 @pytest.mark.parametrize("N,stress,frac", [(10, False, 0.25), (10, True, 0.25), (10, False, 1.0),
-                                            (5, False, 0.25), (16, False, 0.0), (1, False, 0.5)])
+                                            (5, False, 0.25), (16, False, 0.0), (1, False, 0.5),
+                                            (20, False, 1.0), (12, True, 1.0)])
 def test_random_batches_match_reference_live(cm, orc, solver_mod, N, stress, frac):
     if not orc.ref_available():
         pytest.skip("oracle/_ref not present")
