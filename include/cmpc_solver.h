@@ -51,6 +51,35 @@
 
 #define CMPC_MAX_HORIZON  24  /* reference caps at 19 (SolverMPC.cpp:113-116); lifted for N=20 */
 
+/* ------------------------------------------------------------------------------------------ */
+/* Config 5: periodic-disturbance estimation (fp32 words).                                    */
+/* LogData record: the previous step's logged state, forces and model, as the caller receives */
+/* it from /log_data (unitree_legged_msgs/msg/LogData.msg; read at                            */
+/* ConvexMPCLocomotion.cpp:639-771). geometry_msgs doubles are stored as fp32, the precision */
+/* the reference casts them to.                                                               */
+/* ------------------------------------------------------------------------------------------ */
+#define CMPC_LOG_POS      0   /* pos_act x,y,z                                                  */
+#define CMPC_LOG_EUL      3   /* euler_act x,y,z (roll, pitch, yaw)                             */
+#define CMPC_LOG_ANG      6   /* vel_act.angular x,y,z                                          */
+#define CMPC_LOG_LIN      9   /* vel_act.linear x,y,z                                           */
+#define CMPC_LOG_FORCE    12  /* foot_force{0..3}_{x,y,z}, leg-major                            */
+#define CMPC_LOG_XDRAG    24  /* x_drag                                                         */
+#define CMPC_LOG_R        25  /* r_{x,y,z}_{1..4}, axis-major 3x4                               */
+#define CMPC_LOG_ROT      37  /* R_00 .. R_22, row-major                                        */
+#define CMPC_LOG_WORDS    48
+/* Estimator state of one instance: the reference's globals time_history / diff_history /
+ * est_* / f_est (SolverMPC.cpp:390-398, 555-563), with the unbounded histories replaced by a
+ * ring of the last CMPC_EST_WINDOW samples (only that window is ever read). */
+#define CMPC_EST_WINDOW   400 /* window_size (SolverMPC.cpp:704)                                */
+#define CMPC_EST_STOP     500 /* re-estimation stops above this count (SolverMPC.cpp:707)       */
+#define CMPC_EST_F        0   /* f_ext[3] samples, ring [400]                                   */
+#define CMPC_EST_T        400 /* simulation_time samples, ring [400]                            */
+#define CMPC_EST_COUNT    800 /* int32: samples pushed so far (= time_history.size(), capped)   */
+#define CMPC_EST_HEAD     801 /* int32: ring slot of the next sample (= the oldest one)         */
+#define CMPC_EST_FEST3    802 /* f_est(3), the compensation force                               */
+#define CMPC_EST_PARAMS   804 /* double[4]: est_stat, est_amp, est_freq, est_phase              */
+#define CMPC_EST_WORDS    816
+
 /* Per-instance status (batched API). The reference has no status: on qpOASES failure it prints
  * "failed to solve!" and leaves stale forces (SolverMPC.cpp:964-968). Documented deviation:
  * forces are zero when status != CMPC_OK. */
@@ -127,6 +156,19 @@ CMPC_EXTERNC int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int 
  * (row-major) and qg per instance, all variables kept (no swing elimination). */
 CMPC_EXTERNC int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int batch,
                                      float* d_H, float* d_g);
+/* Config 5, one estimator step for every instance (SolverMPC.cpp:688-811 per instance, the
+ * residual of ConvexMPCLocomotion.cpp:639-771 first when d_logs is given):
+ *   f_ext  = residual(d_logs[i], d_records[i])          if d_logs  (written to d_fext6 if set)
+ *            (0, 0, 0, d_fext3[i], 0, 0)                 otherwise
+ *   push (f_ext[3], t_i) into d_est[i], t_i = d_time ? d_time[i] : sim_time;
+ *   400 <= count <= 500: band-pass (Gaussian sigma 7 minus sigma 27), DFT peak, sine fit;
+ *   count >= 400: f_est(3) = est_amp + sin(2 pi t_i est_freq + est_phase);
+ *   d_records[i]: CMPC_REC_FEST3 = f_est(3), CMPC_REC_FLAGS bit 0 = (count > 500).
+ * d_est: batch * CMPC_EST_WORDS words, zero-initialised by the caller before the first step.
+ * Asynchronous on the handle's stream; run it before cmpc_batch_solve on the same records. */
+CMPC_EXTERNC int cmpc_batch_estimate(cmpc_batch* h, float* d_est, const float* d_logs,
+                                     const float* d_fext3, const float* d_time, float sim_time,
+                                     float* d_records, float* d_fext6, int batch);
 /* Measurement hooks: record HIP events around each size-class launch of the next `steps`
  * solves; read back per-launch ms pairs [class1, class2] and class 1's overflow count (the
  * number of instances handed to the 2-wave class in the last solve). Synchronises. */

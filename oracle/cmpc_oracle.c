@@ -12,6 +12,9 @@
 #include <string.h>
 
 #define BIG_NUMBER 5e10f /* SolverMPC.cpp:19 */
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
 
 /* ---------------------------------------------------------------------------------------- */
 /* small dense helpers (row-major)                                                           */
@@ -377,4 +380,156 @@ int oracle_reduce_ws(const float* rec, const cmpc_params* prm, const float* qH, 
 void oracle_scatter(const oracle_red* red, const double* q_red, double* q_soln) {
   int vc = 0;
   for (int i = 0; i < red->nv_full; i++) q_soln[i] = red->var_elim[i] ? 0.0 : q_red[vc++];
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* Config 5: periodic-disturbance estimation                                                 */
+/* ---------------------------------------------------------------------------------------- */
+
+/* gaussian_filter (SolverMPC.cpp:404-437): float kernel of radius ceil(3 sigma), each tap
+ * exp(-0.5 i^2 / sigma^2) evaluated in double and stored as float, normalised by a float sum;
+ * double accumulation with edge clamping. */
+void oracle_gaussian_filter(const double* data, int n, float sigma, double* out) {
+  const int radius = (int)ceil(3 * sigma);
+  float kernel[2 * 81 + 1];
+  float sum = 0.0f;
+  for (int i = -radius; i <= radius; i++) {
+    const float value = (float)exp(-0.5 * (i * i) / (double)(sigma * sigma));
+    kernel[i + radius] = value;
+    sum += value;
+  }
+  for (int i = 0; i < 2 * radius + 1; i++) kernel[i] /= sum;
+  for (int i = 0; i < n; i++) {
+    double acc = 0.0;
+    for (int j = -radius; j <= radius; j++) {
+      int idx = i + j;
+      if (idx < 0) idx = 0;
+      else if (idx >= n) idx = n - 1;
+      acc += data[idx] * kernel[j + radius];
+    }
+    out[i] = acc;
+  }
+}
+
+/* fit_sin (SolverMPC.cpp:478-541): |r2c| of bins 0..n/2 (here a direct DFT in double), argmax
+ * over bins >= 1 (first maximum), freq = |fftfreq(n, tt[1]-tt[0])[k]|, amp = sqrt(2) std,
+ * offset = mean, phase = 0; returned freq = (2 pi f) / (2 pi) as the reference computes it. */
+void oracle_fit_sin(const double* tt, const double* yy, int n, double* amp, double* freq,
+                    double* phase, double* offset, int* peak_bin) {
+  const double dt = tt[1] - tt[0];
+  int max_index = 1;
+  double max_val = -1.0;
+  for (int k = 1; k <= n / 2; k++) {
+    double re = 0.0, im = 0.0;
+    for (int t = 0; t < n; t++) {
+      const double ang = 2.0 * M_PI * (double)((long)k * t % n) / (double)n;
+      re += yy[t] * cos(ang);
+      im -= yy[t] * sin(ang);
+    }
+    const double mag = sqrt(re * re + im * im);
+    if (k == 1 || mag > max_val) { max_val = mag; max_index = k; }
+  }
+  const double guess_freq = fabs((max_index <= n / 2) ? max_index / (n * dt) : (max_index - n) / (n * dt));
+  double m = 0.0;
+  for (int i = 0; i < n; i++) m += yy[i];
+  m /= n;
+  double acc = 0.0;
+  for (int i = 0; i < n; i++) acc += (yy[i] - m) * (yy[i] - m);
+  const double s = sqrt(acc / n);
+  const double w = 2 * M_PI * guess_freq;
+  *amp = s * sqrt(2.0);
+  *offset = m;
+  *phase = 0.0;
+  *freq = w / (2 * M_PI);
+  if (peak_bin) *peak_bin = max_index;
+}
+
+/* Residual f_ext of ConvexMPCLocomotion.cpp:639-771: e = x_k - A_prev x_prev - B_prev u_prev with
+ * the CONTINUOUS model of the logged step (no dt), x(12) = -9.81, u_prev = -logged forces;
+ * f_ext = (-e6, -e7, e8, e9, e10, e11). x_k = (roll, pitch, yaw, p, w, v, -9.81) of the record. */
+void oracle_residual(const float* log, const float* rec, float f_ext[6]) {
+  float A[169], B[156];
+  const float* R = log + CMPC_LOG_ROT; /* R_yaw, row-major */
+  const float Ibody[3] = {0.07f, 0.26f, 0.242f};
+  float RI[9], Iw[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) RI[i * 3 + j] = R[i * 3 + j] * Ibody[j];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      float s = 0.f;
+      for (int k = 0; k < 3; k++) s += RI[i * 3 + k] * R[j * 3 + k];
+      Iw[i * 3 + j] = s;
+    }
+  /* A_prev / B_prev have exactly the ct_ss_mats structure (:641-687 vs SolverMPC.cpp:260-279) */
+  ct_ss_mats(Iw, 12.f, log + CMPC_LOG_R, R, log[CMPC_LOG_XDRAG], A, B);
+  float x_k[13], x_prev[13], u_prev[12];
+  x_k[0] = rec[CMPC_REC_RPY + 0];
+  x_k[1] = rec[CMPC_REC_RPY + 1];
+  x_k[2] = rec[CMPC_REC_RPY + 2];
+  for (int i = 0; i < 3; i++) {
+    x_k[3 + i] = rec[CMPC_REC_P + i];
+    x_k[6 + i] = rec[CMPC_REC_W + i];
+    x_k[9 + i] = rec[CMPC_REC_V + i];
+    x_prev[0 + i] = log[CMPC_LOG_EUL + i];
+    x_prev[3 + i] = log[CMPC_LOG_POS + i];
+    x_prev[6 + i] = log[CMPC_LOG_ANG + i];
+    x_prev[9 + i] = log[CMPC_LOG_LIN + i];
+  }
+  x_k[12] = -9.81f;
+  x_prev[12] = -9.81f;
+  for (int i = 0; i < 12; i++) u_prev[i] = -log[CMPC_LOG_FORCE + i];
+  float e[13];
+  for (int i = 0; i < 13; i++) {
+    float ax = 0.f, bu = 0.f;
+    for (int k = 0; k < 13; k++) ax += A[i * 13 + k] * x_prev[k];
+    for (int k = 0; k < 12; k++) bu += B[i * 12 + k] * u_prev[k];
+    e[i] = (x_k[i] - ax) - bu;
+  }
+  f_ext[0] = -e[6];
+  f_ext[1] = -e[7];
+  f_ext[2] = e[8];
+  f_ext[3] = e[9];
+  f_ext[4] = e[10];
+  f_ext[5] = e[11];
+}
+
+/* Estimator step (SolverMPC.cpp:688-798) on a CMPC_EST_WORDS state. */
+float oracle_est_step(float* st, float f3, float t, int* use_f_est) {
+  int32_t count, head;
+  memcpy(&count, st + CMPC_EST_COUNT, 4);
+  memcpy(&head, st + CMPC_EST_HEAD, 4);
+  double prm[4];
+  memcpy(prm, st + CMPC_EST_PARAMS, sizeof(prm));
+  st[CMPC_EST_F + head] = f3; /* diff_history.push_back(f_ext(3)) */
+  st[CMPC_EST_T + head] = t;  /* time_history.push_back(simulation_time) */
+  head = (head + 1) % CMPC_EST_WINDOW;
+  if (count < (1 << 30)) count++;
+  float f_est3 = st[CMPC_EST_FEST3];
+  if (count >= CMPC_EST_WINDOW) {
+    if (count <= CMPC_EST_STOP) {
+      double tw[CMPC_EST_WINDOW], dw[CMPC_EST_WINDOW], b7[CMPC_EST_WINDOW], b27[CMPC_EST_WINDOW];
+      for (int i = 0; i < CMPC_EST_WINDOW; i++) {
+        const int idx = (head + i) % CMPC_EST_WINDOW; /* oldest first */
+        tw[i] = st[CMPC_EST_T + idx];
+        dw[i] = st[CMPC_EST_F + idx];
+      }
+      oracle_gaussian_filter(dw, CMPC_EST_WINDOW, 7.0f, b7);
+      oracle_gaussian_filter(dw, CMPC_EST_WINDOW, 27.0f, b27);
+      for (int i = 0; i < CMPC_EST_WINDOW; i++) b7[i] = b7[i] - b27[i];
+      double amp, freq, phase, offset;
+      oracle_fit_sin(tw, b7, CMPC_EST_WINDOW, &amp, &freq, &phase, &offset, NULL);
+      prm[0] = offset; /* est_stat */
+      prm[1] = amp;
+      prm[2] = freq;
+      prm[3] = phase;
+    }
+    /* compensatory_force = est_amp + sin(2 pi t f + phase)  ('+' as in :766), float */
+    f_est3 = (float)(prm[1] + sin(2 * M_PI * t * prm[2] + prm[3]));
+  }
+  st[CMPC_EST_FEST3] = f_est3;
+  memcpy(st + CMPC_EST_COUNT, &count, 4);
+  memcpy(st + CMPC_EST_HEAD, &head, 4);
+  memcpy(st + CMPC_EST_PARAMS, prm, sizeof(prm));
+  if (use_f_est) *use_f_est = count > CMPC_EST_STOP;
+  return f_est3;
 }

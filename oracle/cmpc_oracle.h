@@ -64,6 +64,17 @@ int oracle_reduce_ws(const float* rec, const cmpc_params* prm, const float* qH, 
 /* Scatter a reduced solution back to q_soln[12N] (0 for eliminated), SolverMPC.cpp:970-982. */
 void oracle_scatter(const oracle_red* red, const double* q_red, double* q_soln);
 
+/* ---- Config 5: periodic-disturbance estimation ---------------------------------------------
+ * gaussian_filter (SolverMPC.cpp:404-437), fit_sin (:478-541) with the FFTW r2c magnitudes
+ * evaluated by a direct DFT, the estimator step (:688-798) on a CMPC_EST_WORDS state with the
+ * device layout, and the caller's residual (ConvexMPCLocomotion.cpp:639-771). */
+void oracle_gaussian_filter(const double* data, int n, float sigma, double* out);
+void oracle_fit_sin(const double* tt, const double* yy, int n, double* amp, double* freq,
+                    double* phase, double* offset, int* peak_bin);
+void oracle_residual(const float* log, const float* rec, float f_ext[6]);
+/* Pushes (f3, t); returns f_est(3); *use_f_est = (count > 500), the qg switch of :808. */
+float oracle_est_step(float* state, float f3, float t, int* use_f_est);
+
 
 #ifdef __cplusplus
 }

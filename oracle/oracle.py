@@ -60,6 +60,11 @@ def lib():
         _lib = ctypes.CDLL(ORACLE_SO)
         _lib.oracle_condense.argtypes = [_f, ctypes.c_void_p, ctypes.POINTER(OracleCond)]
         _lib.oracle_reduce.argtypes = [_f, ctypes.c_void_p, _f, _f, ctypes.POINTER(OracleRed)]
+        _lib.oracle_gaussian_filter.argtypes = [_d, ctypes.c_int, ctypes.c_float, _d]
+        _lib.oracle_fit_sin.argtypes = [_d, _d, ctypes.c_int, _d, _d, _d, _d, _i]
+        _lib.oracle_residual.argtypes = [_f, _f, _f]
+        _lib.oracle_est_step.argtypes = [_f, ctypes.c_float, ctypes.c_float, _i]
+        _lib.oracle_est_step.restype = ctypes.c_float
     return _lib
 
 
@@ -146,3 +151,43 @@ def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1):
     ref().ref_solve_batch(_fp(records), B, ctypes.byref(prm), q.ctypes.data_as(_d),
                           st.ctypes.data_as(_i), nw.ctypes.data_as(_i), int(nthreads))
     return q, st, nw
+
+
+# ---- config 5: periodic-disturbance estimation (SolverMPC.cpp:404-553, 688-811) ------------
+EST_WORDS = 816      # CMPC_EST_WORDS
+LOG_WORDS = 48       # CMPC_LOG_WORDS
+
+
+def gaussian_filter(data: np.ndarray, sigma: float) -> np.ndarray:
+    data = np.ascontiguousarray(data, np.float64)
+    out = np.zeros_like(data)
+    lib().oracle_gaussian_filter(data.ctypes.data_as(_d), data.size, float(sigma),
+                                 out.ctypes.data_as(_d))
+    return out
+
+
+def fit_sin(tt: np.ndarray, yy: np.ndarray):
+    """-> (amp, freq, phase, offset, peak_bin) as SolverMPC.cpp:478-541 (direct DFT)."""
+    tt = np.ascontiguousarray(tt, np.float64)
+    yy = np.ascontiguousarray(yy, np.float64)
+    o = [ctypes.c_double() for _ in range(4)]
+    k = ctypes.c_int()
+    lib().oracle_fit_sin(tt.ctypes.data_as(_d), yy.ctypes.data_as(_d), tt.size,
+                         *[ctypes.byref(x) for x in o], ctypes.byref(k))
+    return o[0].value, o[1].value, o[2].value, o[3].value, k.value
+
+
+def residual(log: np.ndarray, rec: np.ndarray) -> np.ndarray:
+    """f_ext[6] of ConvexMPCLocomotion.cpp:639-771 from a LogData record + the current record."""
+    out = np.zeros(6, np.float32)
+    lib().oracle_residual(_fp(np.ascontiguousarray(log, np.float32)),
+                          _fp(np.ascontiguousarray(rec, np.float32)), _fp(out))
+    return out
+
+
+def est_step(state: np.ndarray, f3: float, t: float):
+    """One estimator step in place on a [EST_WORDS] float32 state -> (f_est3, use_f_est)."""
+    assert state.dtype == np.float32 and state.flags["C_CONTIGUOUS"] and state.size == EST_WORDS
+    use = ctypes.c_int()
+    f = lib().oracle_est_step(_fp(state), float(f3), float(t), ctypes.byref(use))
+    return f, bool(use.value)

@@ -19,9 +19,11 @@ LIB = os.path.join(PKG, "libcmpc_hip.so")
 OBJ = os.path.join(ROOT, "build", "obj")
 # one translation unit per kernel family so the large unrolled kernels compile in parallel
 SOURCES = ["cmpc_class1.hip", "cmpc_class2.hip", "cmpc_classg.hip", "cmpc_launch.hip",
-           "cmpc_abi.cpp"]
+           "cmpc_estimator.hip", "cmpc_abi.cpp"]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
+# -fno-slp-vectorize: the SLP pass packs adjacent row updates into v_pk_fma_f32, which ties
+# slot registers into 64-bit pairs and made the register-resident rows spill
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", "-fno-slp-vectorize"]
 
 
 def _deps(path: str, seen=None) -> set:

@@ -35,6 +35,7 @@ struct cmpc_batch {
   bool own_stream = false;
   int* d_work = nullptr;
   float* d_gscratch = nullptr;   // slabs of the general size class (cmpc_classg.hip)
+  float* d_gauss = nullptr;      // gaussian_filter kernels of the config-5 estimator
   size_t gscratch_floats = 0;
   // staging for the host-pointer entry point (allocated lazily, sized max_batch)
   float* d_rec = nullptr;
@@ -60,6 +61,18 @@ static cmpc::KParams make_kparams(const cmpc_params& p) {
 }
 
 extern "C" int cmpc_record_words(int horizon) { return CMPC_REC_WORDS(horizon); }
+
+// The float kernel of gaussian_filter (SolverMPC.cpp:404-418): taps exp(-0.5 i^2 / sigma^2)
+// evaluated in double, stored as float, normalised by their float sum.
+static void gauss_kernel(float sigma, int radius, float* out) {
+  float sum = 0.0f;
+  for (int i = -radius; i <= radius; i++) {
+    const float value = std::exp(-0.5 * (i * i) / (sigma * sigma));
+    out[i + radius] = value;
+    sum += value;
+  }
+  for (int i = 0; i < 2 * radius + 1; i++) out[i] /= sum;
+}
 
 extern "C" const char* cmpc_last_error(void) { return g_last_error.c_str(); }
 
@@ -107,6 +120,14 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
   }
   e = hipMalloc(&h->d_work, sizeof(int) * cmpc::work_ints(max_batch));
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("hipMalloc(work)", e); }
+  {
+    float taps[cmpc::kGaussTaps];
+    gauss_kernel(7.0f, cmpc::kGaussR7, taps);
+    gauss_kernel(27.0f, cmpc::kGaussR27, taps + 2 * cmpc::kGaussR7 + 1);
+    e = hipMalloc(&h->d_gauss, sizeof(taps));
+    if (e == hipSuccess) e = hipMemcpy(h->d_gauss, taps, sizeof(taps), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("gauss taps", e); }
+  }
   if (int r = ensure_gscratch(h); r != 0) { cmpc_batch_destroy(h); return r; }
   *out = h;
   return 0;
@@ -116,6 +137,7 @@ extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (!h) return;
   if (h->d_work) (void)hipFree(h->d_work);
   if (h->d_gscratch) (void)hipFree(h->d_gscratch);
+  if (h->d_gauss) (void)hipFree(h->d_gauss);
   if (h->d_rec) (void)hipFree(h->d_rec);
   if (h->d_forces) (void)hipFree(h->d_forces);
   if (h->d_status) (void)hipFree(h->d_status);
@@ -139,6 +161,20 @@ extern "C" int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int batch
   hipError_t e = cmpc::launch_solve(d_records, batch, h->kp, d_forces, d_status, d_iters, h->d_work,
                                     h->max_batch, h->d_gscratch, h->stream, ev);
   if (e != hipSuccess) return fail("launch_solve", e);
+  return 0;
+}
+
+extern "C" int cmpc_batch_estimate(cmpc_batch* h, float* d_est, const float* d_logs,
+                                   const float* d_fext3, const float* d_time, float sim_time,
+                                   float* d_records, float* d_fext6, int batch) {
+  if (!h || batch < 0 || batch > h->max_batch || (batch && (!d_est || !d_records)) ||
+      (batch && !d_logs && !d_fext3)) {
+    g_last_error = "cmpc_batch_estimate: bad arguments";
+    return -1;
+  }
+  hipError_t e = cmpc::launch_estimate(d_est, d_logs, d_fext3, d_time, sim_time, d_records,
+                                       h->kp.rec_words, d_fext6, h->d_gauss, batch, h->stream);
+  if (e != hipSuccess) return fail("launch_estimate", e);
   return 0;
 }
 

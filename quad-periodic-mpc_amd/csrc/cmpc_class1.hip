@@ -346,7 +346,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       const Cons cp = decode_cons(p, mui, sh.sub[p / 6]);
       float up = 0.f;
       for (;;) {
-        if (++iters > P.max_iter) { status = CMPC_MAX_ITER; break; }
+        if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
         pin(slot);
         // d = J' n+ : rows ia, iz of J through LDS
         if (v == cp.ia && cp.ia != cp.iz) {
@@ -410,8 +410,8 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           // ---- add p: Givens rotations zeroing d[q+1..n-1] into d[q]; parameters in closed
           // form from suffix norms ts_j = |d[j..n-1]|
           const float ts = sqrtf(wave_suffix_sum((v >= q && v < n) ? dv * dv : 0.f, v));
-          const float ts_prev = __shfl_up(ts, 1, 64);
-          const float d_prev = __shfl_up(dv, 1, 64);
+          const float ts_prev = lane_prev(ts, ts);
+          const float d_prev = lane_prev(dv, dv);
           float cj = 1.f, sj = 0.f;
           if (v > q && v < n && ts_prev > 0.f) {
             const float ri = fast_rcp(ts_prev);
@@ -441,8 +441,8 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           const int k = __builtin_amdgcn_readfirstlane(kk);
           const int ak = rli(act_reg, k);
           if (v == 0) sh.cflag[ak] = 0;
-          const int a_nx = __shfl_down(act_reg, 1, 64);
-          const float u_nx = __shfl_down(u_reg, 1, 64);
+          const int a_nx = lane_next_i(act_reg, act_reg);
+          const float u_nx = lane_next(u_reg, u_reg);
           if (v >= k && v < q - 1) { act_reg = a_nx; u_reg = u_nx; }
           static_for<0, NV - 1>([&](auto JC) {
             constexpr int j = decltype(JC)::value;  // 0 .. NV-2

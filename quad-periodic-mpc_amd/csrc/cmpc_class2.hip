@@ -1,34 +1,591 @@
-// cmpc_class2.hip — register-resident size class W=2 (n <= 128 reduced variables)
-#include "cmpc_device.h"
+// cmpc_class2.hip — size class 2: fused condensation + friction-cone QP for instances with
+// 64 < n <= 128 reduced force variables (random contact tables at N = 10, trot at N = 11..21),
+// one 128-lane workgroup (two wavefronts) per instance, over class 1's overflow list.
+//
+// Same computation as cmpc_class1.hip — one call of the reference's solve_mpc()
+// (be2r_cmpc_unitree/src/controllers/convexMPC/SolverMPC.cpp:566-982) — with the same mapping:
+// lane v owns reduced variable v (row v of H, of the Cholesky working matrix, then of J = L^-T,
+// in 129 VGPRs), the packed upper-row LDS matrix P holds H and then the raw Cholesky columns.
+// What changes with two wavefronts:
+//   * each Cholesky step publishes its pivot column (slot[k] of every lane) and crosses ONE
+//     s_barrier; J = L^-T and x = -J y only read LDS, so they run barrier-free;
+//   * the QP's triangular factor R is kept EXPLICITLY, as packed upper columns in the region
+//     that held L (dead once J is formed). The back substitution r = R^-1 d1 and the
+//     re-triangularisation after a drop then run inside wavefront 0 with readlanes only, where
+//     the implicit R of class 1 would need a cross-wave reduction per active constraint;
+//   * cross-wave scalars (|x| max, |d|^2, the dual step) go through a few LDS words.
+// Everything is fp32 (the reference condenses in fp32: common_types.h:14).
+#include "cmpc_common.h"
+
+#ifndef CMPC_W2_WAVES_PER_EU
+#define CMPC_W2_WAVES_PER_EU 2
+#endif
 
 namespace cmpc {
+namespace {
 
-#ifndef CMPC_W1_WAVES_PER_EU
-#define CMPC_W1_WAVES_PER_EU 2  // 2 waves/SIMD: measured best (r01: 6.1 ms vs 10.2 at 1, 9.5 at 3 with spills)
-#endif
-// Register-resident size classes. Class W handles instances with n <= 64 W reduced variables;
-// class 1 runs one workgroup per instance over the batch, wider classes run a persistent grid
-// over the overflow list of the previous class.
-template <int W>
-__global__ __launch_bounds__(64 * W, (W == 1 ? CMPC_W1_WAVES_PER_EU : 1)) void cmpc_solve_reg_kernel(
-    const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
-    uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
-    const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
-  __shared__ SharedReg<W> sh;
-  const int count = in_list ? *in_count : batch;
-  for (int t = blockIdx.x; t < count; t += gridDim.x) {
-    const int inst = in_list ? in_list[t] : t;
-    solve_reg<W>(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
-                 status + inst, iters ? iters + inst : nullptr, ovf_list, ovf_count, inst);
-    __syncthreads();
+constexpr int NV = 128;
+constexpr int NG = NV / 4;
+constexpr int PSZ = 4 * NG * NV - 8 * NG * (NG - 1);  // packed rows r: columns [r & ~3, NV)
+constexpr int kNone = 0x7fffffff;
+
+__host__ __device__ constexpr int prow(int r) {
+  return 4 * (r >> 2) * NV - 8 * (r >> 2) * ((r >> 2) - 1) + (r & 3) * (NV - 4 * (r >> 2));
+}
+__host__ __device__ constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+// R (upper triangular, q x q) packed by columns: R[i][j] at rcol(j) + i, i <= j
+__device__ __forceinline__ int rcol(int j) { return (j * (j + 1)) >> 1; }
+static_assert(NV * (NV + 1) / 2 <= PSZ, "R must fit in P");
+
+constexpr int OFF_TRAJ = 0;
+constexpr int OFF_E = 12 * MAXN;
+constexpr int OFF_ZE = OFF_E + 16 * MAXN;
+static_assert(OFF_ZE + 16 * MAXN <= PSZ, "prep scratch must fit in P");
+
+// 40.2 KB: four workgroups (eight wavefronts) per CU, matching the 256-VGPR budget
+struct SharedC2 {
+  float P[PSZ];
+  float BdtT[12][16];
+  float ibuf[NV];          // 1 / sqrt(d_k) of pivot k
+  float vbuf[NV];          // y, then the masked d (v >= q, v < n)
+  float dfull[NV];         // d = J' n+
+  float bufA[NV], bufB[NV];  // gradient border of pivot k (Cholesky); J rows ia, iz (QP)
+  float xs[NV];
+  float cs[2 * NV];        // Givens (c, s) per column pair
+  float redf[8];
+  int redi[8];
+  float sub[4 * MAXN];     // ub of each stance foot-step (gait * f_max)
+  int sfs[4 * MAXN];       // stance foot-step ids, in order
+  int blkbase[MAXN + 2];   // first reduced variable of each horizon step
+  unsigned char varblk[NV], varcol[NV];
+  unsigned char stance[4 * MAXN];
+  unsigned char cflag[2 * NV + 8];  // active flag per constraint id (6 per stance foot-step)
+};
+
+__device__ __forceinline__ void bar() { __syncthreads(); }
+// compiler-only ordering point for LDS traffic inside one wavefront
+__device__ __forceinline__ void lsync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ float fdiv(float a, float b) { return a * fast_rcp(b); }
+
+template <int M>
+__device__ __forceinline__ void pin(float (&x)[M]) {
+#pragma unroll
+  for (int c = 0; c < M; c++) asm volatile("" : "+v"(x[c]));
+}
+
+#define CMPC_SWEEP_FENCE(c)                                  \
+  do {                                                       \
+    if (((c) & 15) == 12) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
+__device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KParams& P,
+                                         SharedC2& sh, float* __restrict__ fout,
+                                         uint8_t* __restrict__ st_out, int32_t* __restrict__ it_out,
+                                         int* __restrict__ ovf_list, int* __restrict__ ovf_count,
+                                         int inst) {
+  const int v = threadIdx.x;
+  const int lane = v & 63;
+  const int wave = v >> 6;
+  const int N = P.N;
+  // ---- stance table + elimination (SolverMPC.cpp:869-894): both wavefronts compact it (same
+  // result), wavefront 0 stores it
+  const unsigned char* gait = reinterpret_cast<const unsigned char*>(rec + CMPC_REC_HDR + 12 * N);
+  int nfs = 0;
+  for (int c0 = 0; c0 < 4 * N; c0 += 64) {
+    const int t = c0 + lane;
+    float ub = 0.f;
+    bool f = false;
+    if (t < 4 * N) {
+      ub = (float)gait[t] * P.f_max;
+      f = !(ub < 0.01f && ub > -0.01f);
+      if (wave == 0) sh.stance[t] = f ? 1 : 0;
+    }
+    const unsigned long long m = __ballot(f);
+    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (f && wave == 0) {
+      sh.sfs[nfs + pre] = t;
+      sh.sub[nfs + pre] = ub;
+    }
+    nfs += __popcll(m);
+  }
+  const int n = 3 * nfs;
+  if (n > NV) {  // hand the instance to the general class
+    if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
+    return;
+  }
+  bar();
+  {
+    int kb = 0, kc = 0;
+    if (v < n) {
+      const int fs = sh.sfs[v / 3];
+      kb = fs >> 2;
+      kc = 3 * (fs & 3) + v % 3;
+    }
+    sh.varblk[v] = (unsigned char)kb;
+    sh.varcol[v] = (unsigned char)kc;
+    if (v <= N) {
+      int c = 0;
+      for (int s = 0; s < nfs; s++) c += (sh.sfs[s] < 4 * v) ? 1 : 0;
+      sh.blkbase[v] = 3 * c;
+    }
+    for (int t = v; t < 6 * nfs; t += NV) sh.cflag[t] = 0;
+    for (int t = v; t < 12 * N; t += NV) sh.P[OFF_TRAJ + t] = rec[CMPC_REC_HDR + t];
+  }
+  Model md;
+  make_model(rec, P.dt, md);
+  make_bdt<NV>(rec, md, v, sh.BdtT);
+  bar();
+  if (v < N) {
+    float e[13];
+    state_error(rec, md, v, &sh.P[OFF_TRAJ + 12 * v], e);
+#pragma unroll
+    for (int j = 0; j < 13; j++) sh.P[OFF_E + 16 * v + j] = e[j];
+  }
+  bar();
+  float wts[13];
+#pragma unroll
+  for (int j = 0; j < 12; j++) wts[j] = P.wts[j];
+  wts[12] = 0.f;
+  // gradient recursion ze_i = S e_i + Adt' ze_{i+1} (uniform; lane j < 13 stores component j)
+  {
+    float ze[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) ze[j] = 0.f;
+    for (int i = N - 1; i >= 0; i--) {
+      float e[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) e[j] = sh.P[OFF_E + 16 * i + j];
+      recur(md, wts, e, ze);
+      float mine = 0.f;
+#pragma unroll
+      for (int j = 0; j < 13; j++) mine = (v == j) ? ze[j] : mine;
+      if (v < 13) sh.P[OFF_ZE + 16 * i + v] = mine;
+    }
+  }
+  bar();
+
+  // ---- condensation: lane v builds H[v][w] for w >= v into packed P, and its gradient g_v
+  const bool real = v < n;
+  float gv;
+  {
+    const int kv = real ? sh.varblk[v] : 0;
+    const int cv = real ? sh.varcol[v] : 0;
+    float b[13], u1[13], u2[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) b[j] = real ? sh.BdtT[cv][j] : 0.f;
+    n1_mul(md, b, u1);
+    n1_mul(md, u1, u2);
+    {
+      float zk[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) zk[j] = sh.P[OFF_ZE + 16 * kv + j];
+      gv = real ? 2.f * dot13(b, zk) : 0.f;  // qg = 2 B_qp' S (A_qp x0 + Q_qp f - X_d)
+    }
+    bar();  // every ZE read is done before P is overwritten
+    const int myrow = prow0(v);
+    float z[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) z[j] = 0.f;
+    for (int i = N - 1; i >= 0; i--) {
+      // z_i = S Adt^{i-kv} b_v + Adt' z_{i+1}  (the S term only for i >= kv)
+      const bool act = real && (i >= kv);
+      const float k = (float)(i - kv);
+      const float k2 = 0.5f * k * (k - 1.f);
+      float gk[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) gk[j] = act ? fmaf(k2, u2[j], fmaf(k, u1[j], b[j])) : 0.f;
+      recur(md, wts, gk, z);
+      const int wb = __builtin_amdgcn_readfirstlane(sh.blkbase[i]);
+      const int we = __builtin_amdgcn_readfirstlane(sh.blkbase[i + 1]);
+      for (int w = wb; w < we; w++) {
+        const int cw = sh.varcol[w];
+        float bw[13];
+#pragma unroll
+        for (int j = 0; j < 13; j++) bw[j] = sh.BdtT[cw][j];
+        float val = 2.f * dot13(bw, z);
+        if (w == v) val += P.alpha2;  // qH = 2 (B'SB + alpha I), SolverMPC.cpp:806
+        if (act && w >= v) sh.P[myrow + w] = val;
+      }
+    }
+  }
+  bar();
+
+  // ---- row v of H into registers (full symmetric; identity padding for v >= n) ----------
+  float slot[NV + 1];
+  {
+    const int myrow = prow0(v);
+    static_for<0, NV>([&](auto C) {
+      constexpr int c = decltype(C)::value;
+      const int addr = (c >= v) ? myrow + c : prow0(c) + v;
+      const float x = sh.P[addr];
+      slot[c] = (real && c < n) ? x : ((c == v) ? 1.f : 0.f);
+      if ((c & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    });
+    slot[NV] = gv;
+  }
+  bar();
+
+  // ---- bordered Cholesky [H | g]: raw column k = slot[k] of every lane -> P row k ----------
+  int status = CMPC_OK;
+  float my_inv = 1.f;
+  static_for<0, NV>([&](auto KC) {
+    constexpr int k = decltype(KC)::value;
+    constexpr int c0 = k & ~3;
+    constexpr int rk = prow(k);
+    if (k < n) {
+      if (v >= c0) sh.P[rk + v - c0] = (v >= k) ? slot[k] : 0.f;
+      if (v == k) sh.bufA[k] = slot[NV];
+      bar();
+      float d = sh.P[rk + k - c0];
+      if (!(d > 0.f)) { status = CMPC_NOT_PD; d = 1e-30f; }
+      const float inv = rsqrtf(d);
+      if (v == k) { my_inv = inv; sh.ibuf[k] = inv; }
+      const float a = (v > k) ? -slot[k] * (inv * inv) : 0.f;
+#pragma unroll
+      for (int c = c0; c < NV; c += 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
+        slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
+        slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
+        slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
+        slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+        CMPC_SWEEP_FENCE(c);
+      }
+      slot[NV] = fmaf(a, sh.bufA[k], slot[NV]);
+      pin(slot);
+    }
+  });
+  const float yv = (v < n) ? slot[NV] * my_inv : 0.f;  // L y = g
+  bar();
+
+  // ---- J = L^-T: lane v solves L x = e_v (column v of L^-1 = row v of J); LDS reads only ----
+  static_for<0, NV>([&](auto C) {
+    constexpr int c = decltype(C)::value;
+    slot[c] = (c == v) ? 1.f : 0.f;
+  });
+  static_for<0, NV>([&](auto KC) {
+    constexpr int k = decltype(KC)::value;
+    constexpr int c0 = k & ~3;
+    constexpr int rk = prow(k);
+    if (k < n) {
+      lsync();
+      const float inv = sh.ibuf[k];
+      const float xk = slot[k] * inv;
+      const float a = -xk * inv;
+#pragma unroll
+      for (int c = c0; c < NV; c += 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
+        slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
+        slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
+        slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
+        slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+        CMPC_SWEEP_FENCE(c);
+      }
+      slot[k] = xk;
+      pin(slot);
+    }
+  });
+
+  // ---- unconstrained minimiser x = -J y ----------------------------------------------------
+  sh.vbuf[v] = yv;
+  bar();
+  float xv = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; c += 4) {
+    const float4 y4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+    xv = fmaf(slot[c + 0], y4.x, xv);
+    xv = fmaf(slot[c + 1], y4.y, xv);
+    xv = fmaf(slot[c + 2], y4.z, xv);
+    xv = fmaf(slot[c + 3], y4.w, xv);
+    CMPC_SWEEP_FENCE(c);
+  }
+  xv = (v < n) ? -xv : 0.f;
+  bar();  // L (in P) and y are dead from here; P holds R
+
+  // ---- Goldfarb-Idnani dual active set on the friction pyramids -----------------------------
+  const float mui = P.mu_inv;
+  const float fnorm = rsqrtf(mui * mui + 1.f);
+  int q = 0;
+  int iters = 0;
+  // wavefront 0, lane l: active-set positions l and l + 64 (dual u, constraint id, dual step r)
+  float u_lo = 0.f, u_hi = 0.f, r_lo = 0.f, r_hi = 0.f;
+  int a_lo = 0, a_hi = 0;
+  if (status == CMPC_OK) {
+    for (;;) {
+      // lane ids re-materialised per iteration (tid_opq): keeps per-lane LDS addresses out of
+      // the loop preheader, where they would be spilled
+      const int v = tid_opq();
+      const int lane = v & 63;
+      sh.xs[v] = xv;
+      {
+        const float wm = wave_max(fabsf(xv));
+        if (lane == 0) sh.redf[wave] = wm;
+      }
+      bar();
+      // most violated constraint (normalised slack): both wavefronts scan the same foot-steps
+      float best = 0.f;
+      int bid = kNone;
+      if (lane < nfs) {
+        const float fx = sh.xs[3 * lane], fy = sh.xs[3 * lane + 1], fz = sh.xs[3 * lane + 2];
+        float sl[6];
+        sl[0] = (mui * fx + fz) * fnorm;
+        sl[1] = (-mui * fx + fz) * fnorm;
+        sl[2] = (mui * fy + fz) * fnorm;
+        sl[3] = (-mui * fy + fz) * fnorm;
+        sl[4] = fz;
+        sl[5] = sh.sub[lane] - fz;
+#pragma unroll
+        for (int t = 0; t < 6; t++)
+          if (!sh.cflag[6 * lane + t] && sl[t] < best) { best = sl[t]; bid = 6 * lane + t; }
+      }
+      const float xmax = fmaxf(sh.redf[0], sh.redf[1]);
+      wave_argmin(best, bid);
+      const float tol = 1e-5f * fmaxf(1.f, xmax);
+      if (bid == kNone || best >= -tol) break;
+
+      const int p = __builtin_amdgcn_readfirstlane(bid);
+      const Cons cp = decode_cons(p, mui, sh.sub[p / 6]);
+      float up = 0.f;
+      for (;;) {
+        if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
+        pin(slot);
+        const int v = tid_opq();
+        const int lane = v & 63;
+        // d = J' n+ : rows ia, iz of J through LDS
+        // (dword stores: 128-bit stores would tie slot[] into register quads and spill)
+        if (v == cp.ia && cp.ia != cp.iz) {
+#pragma unroll
+          for (int c = 0; c < NV; c++) sh.bufA[c] = slot[c];
+        }
+        if (v == cp.iz) {
+#pragma unroll
+          for (int c = 0; c < NV; c++) sh.bufB[c] = slot[c];
+        }
+        sh.xs[v] = xv;
+        bar();
+        const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[v], cp.cb * sh.bufB[v]) : cp.cb * sh.bufB[v];
+        const float dm = (v >= q && v < n) ? dv : 0.f;
+        sh.vbuf[v] = dm;
+        sh.dfull[v] = dv;
+        {
+          const float dw = wave_sum((v < n) ? dv * dv : 0.f);
+          if (lane == 0) sh.redf[2 + wave] = dw;
+        }
+        const float spv = fmaf(cp.ca, sh.xs[cp.ia], fmaf(cp.cb, sh.xs[cp.iz], -cp.bp));
+        bar();
+        // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+ (split at lane 64), dn = |d|^2
+        float zv = 0.f, zlo = 0.f, zhi = 0.f;
+#pragma unroll
+        for (int c = 0; c < NV; c += 4) {
+          const float4 m4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+          zv = fmaf(slot[c + 0], m4.x, zv);
+          zv = fmaf(slot[c + 1], m4.y, zv);
+          zv = fmaf(slot[c + 2], m4.z, zv);
+          zv = fmaf(slot[c + 3], m4.w, zv);
+          const float s4 = m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
+          if (c < 64) zlo += s4; else zhi += s4;
+          CMPC_SWEEP_FENCE(c);
+        }
+        const float zn = zlo + zhi;
+        const float dn = sh.redf[2] + sh.redf[3];
+        // r = R^-1 d1 by back substitution over the packed columns of R (wavefront 0), then the
+        // partial (dual) step t1 = min_{r_j > 0} u_j / r_j
+        if (wave == 0) {
+          float acc_lo = dv;
+          float acc_hi = sh.dfull[lane + 64];
+          for (int i = q - 1; i >= 0; i--) {
+            const int off = rcol(i);
+            const float rii = sh.P[off + i];
+            const float ai = (i < 64) ? rl(acc_lo, i) : rl(acc_hi, i - 64);
+            const float ri = fdiv(ai, rii);
+            if (lane < i) acc_lo = fmaf(-sh.P[off + lane], ri, acc_lo);
+            if (lane + 64 < i) acc_hi = fmaf(-sh.P[off + lane + 64], ri, acc_hi);
+            r_lo = (lane == i) ? ri : r_lo;
+            r_hi = (lane + 64 == i) ? ri : r_hi;
+          }
+          float t1w = kBigF;
+          int kw = kNone;
+          if (lane < q && r_lo > 0.f) { t1w = fmaxf(fdiv(u_lo, r_lo), 0.f); kw = lane; }
+          if (lane + 64 < q && r_hi > 0.f) {
+            const float th = fmaxf(fdiv(u_hi, r_hi), 0.f);
+            if (th < t1w) { t1w = th; kw = lane + 64; }
+          }
+          wave_argmin(t1w, kw);
+          if (lane == 0) { sh.redf[4] = t1w; sh.redi[4] = kw; }
+        }
+        bar();
+        const float t1 = sh.redf[4];
+        const int kk = __builtin_amdgcn_readfirstlane(sh.redi[4]);
+        const bool zero_step = !(zn > 1e-9f * dn);
+        const float t2 = zero_step ? kBigF : -fdiv(spv, zn);
+        const float t = fminf(t1, t2);
+        if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
+        if (wave == 0) {
+          if (lane < q) u_lo = fmaf(-t, r_lo, u_lo);
+          if (lane + 64 < q) u_hi = fmaf(-t, r_hi, u_hi);
+        }
+        up += t;
+        if (!zero_step) xv = fmaf(t, zv, xv);
+        if (!zero_step && t2 <= t1) {
+          // ---- add p: Givens rotations zeroing d[q+1..n-1] into d[q]; parameters in closed
+          // form from the suffix norms ts_j = |d[j..n-1]|
+          float ss = wave_suffix_sum(dm * dm, lane);
+          if (wave == 0) ss += zhi;
+          const float ts = sqrtf(ss);
+          float cj = 1.f, sj = 0.f;
+          if (v > q && v < n) {
+            const float dprev = sh.vbuf[v - 1];
+            const float tp2 = fmaf(dprev, dprev, ss);  // ts_{v-1}^2
+            if (tp2 > 0.f) {
+              const float ri = rsqrtf(tp2);
+              cj = dprev * ri;
+              sj = ((v == n - 1) ? dv : ts) * ri;
+            }
+          }
+          *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(cj, sj);
+          // new column q of R: R[v][q] = d_v (v < q), R[q][q] = ts_q (d_q when q = n - 1)
+          {
+            const int offq = rcol(q);
+            if (v < q) sh.P[offq + v] = dv;
+            if (v == q) sh.P[offq + q] = (q == n - 1) ? dv : ts;
+          }
+          bar();
+          static_for<0, NV - 1>([&](auto IC) {
+            constexpr int j = NV - 1 - decltype(IC)::value;  // NV-1 .. 1
+            if ((j & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+            if ((unsigned)(j - q - 1) < (unsigned)(n - q - 1)) {  // q < j < n
+              const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+              const float a0 = slot[j - 1], b0 = slot[j];
+              slot[j - 1] = fmaf(cs2.x, a0, cs2.y * b0);
+              slot[j] = fmaf(-cs2.y, a0, cs2.x * b0);
+            }
+          });
+          pin(slot);
+          if (wave == 0) {
+            if (lane == q) { u_lo = up; a_lo = p; }
+            if (lane + 64 == q) { u_hi = up; a_hi = p; }
+          }
+          if (v == 0) sh.cflag[p] = 1;
+          q++;
+          break;
+        }
+        // ---- drop active constraint kk: shift positions kk+1..q-1 down, remove column kk of R
+        // and re-triangularise rows kk..q-1 with Givens rotations (wavefront 0, in place)
+        {
+          const int k = kk;
+          if (wave == 0) {
+            const int ak = (k < 64) ? rli(a_lo, k) : rli(a_hi, k - 64);
+            if (lane == 0) sh.cflag[ak] = 0;
+            const int alo_nx = lane_next_i(a_lo, a_lo);
+            const float ulo_nx = lane_next(u_lo, u_lo);
+            const int ahi_nx = lane_next_i(a_hi, a_hi);
+            const float uhi_nx = lane_next(u_hi, u_hi);
+            const int ahi0 = rli(a_hi, 0);
+            const float uhi0 = rl(u_hi, 0);
+            if (lane >= k && lane < q - 1) {
+              a_lo = (lane == 63) ? ahi0 : alo_nx;
+              u_lo = (lane == 63) ? uhi0 : ulo_nx;
+            }
+            if (lane + 64 >= k && lane + 64 < q - 1) { a_hi = ahi_nx; u_hi = uhi_nx; }
+            // new column c (k <= c <= q-2) = old column c+1. Lane l handles c = l and l + 64.
+            // Every read of an old entry precedes, in this wavefront's LDS order, the write that
+            // reuses its word (new column c overlays old column c).
+            const int clo = lane, chi = lane + 64;
+            const bool in_lo = clo >= k && clo <= q - 2;
+            const bool in_hi = chi >= k && chi <= q - 2;
+            float top_lo = in_lo ? sh.P[rcol(clo + 1) + k] : 0.f;
+            float top_hi = in_hi ? sh.P[rcol(chi + 1) + k] : 0.f;
+            lsync();
+            for (int r = 0; r < k; r++) {
+              const float xlo = in_lo ? sh.P[rcol(clo + 1) + r] : 0.f;
+              const float xhi = in_hi ? sh.P[rcol(chi + 1) + r] : 0.f;
+              lsync();
+              if (in_lo) sh.P[rcol(clo) + r] = xlo;
+              if (in_hi) sh.P[rcol(chi) + r] = xhi;
+              lsync();
+            }
+            for (int j = k; j <= q - 2; j++) {
+              const bool on_lo = in_lo && clo >= j, on_hi = in_hi && chi >= j;
+              const float bot_lo = on_lo ? sh.P[rcol(clo + 1) + j + 1] : 0.f;
+              const float bot_hi = on_hi ? sh.P[rcol(chi + 1) + j + 1] : 0.f;
+              lsync();
+              const float a0 = (j < 64) ? rl(top_lo, j) : rl(top_hi, j - 64);
+              const float b0 = (j < 64) ? rl(bot_lo, j) : rl(bot_hi, j - 64);
+              const float h = sqrtf(a0 * a0 + b0 * b0);
+              float cc = 1.f, sn = 0.f;
+              if (h > 0.f) { const float ih = fast_rcp(h); cc = a0 * ih; sn = b0 * ih; }
+              if (on_lo) {
+                sh.P[rcol(clo) + j] = fmaf(cc, top_lo, sn * bot_lo);
+                top_lo = fmaf(-sn, top_lo, cc * bot_lo);
+              }
+              if (on_hi) {
+                sh.P[rcol(chi) + j] = fmaf(cc, top_hi, sn * bot_hi);
+                top_hi = fmaf(-sn, top_hi, cc * bot_hi);
+              }
+              if (lane == 0) *reinterpret_cast<float2*>(&sh.cs[2 * j]) = make_float2(cc, sn);
+              lsync();
+            }
+          }
+          bar();
+          // the same rotations on J columns (j, j+1), j = k .. q-2
+          static_for<0, NV - 1>([&](auto JC) {
+            constexpr int j = decltype(JC)::value;  // 0 .. NV-2
+            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+            if ((unsigned)(j - k) < (unsigned)(q - 1 - k)) {  // k <= j < q-1
+              const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+              const float x0 = slot[j], x1 = slot[j + 1];
+              slot[j] = fmaf(cs2.x, x0, cs2.y * x1);
+              slot[j + 1] = fmaf(-cs2.y, x0, cs2.x * x1);
+            }
+          });
+          pin(slot);
+          q--;
+        }
+      }
+      if (status != CMPC_OK) break;
+    }
+  }
+
+  // ---- scatter (q_soln layout 12 k + 3 leg + axis, swing -> 0) staged in LDS, coalesced out
+  const bool ok = (status == CMPC_OK);
+  bar();
+  for (int t = v; t < 12 * N; t += NV) sh.P[t] = 0.f;
+  bar();
+  if (ok && v < n) sh.P[12 * sh.varblk[v] + sh.varcol[v]] = xv;
+  bar();
+  for (int t = 4 * v; t < 12 * N; t += 4 * NV)
+    *reinterpret_cast<float4*>(&fout[t]) = *reinterpret_cast<const float4*>(&sh.P[t]);
+  if (v == 0) {
+    st_out[0] = (uint8_t)status;
+    if (it_out) it_out[0] = iters;
   }
 }
 
+}  // namespace
+
+// One workgroup per entry of class 1's overflow list; the grid is sized for the worst case
+// (the list length is only known on the device) and surplus workgroups exit at once.
+__global__ __launch_bounds__(NV, CMPC_W2_WAVES_PER_EU) void cmpc_solve_c2_kernel(
+    const float* __restrict__ recs, KParams P, float* __restrict__ forces,
+    uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
+    const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
+  __shared__ SharedC2 sh;
+  const int t = blockIdx.x;
+  if (t >= *in_count) return;
+  const int inst = in_list[t];
+  solve_c2(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
+           status + inst, iters ? iters + inst : nullptr, ovf_list, ovf_count, inst);
+}
+
 hipError_t launch_class2(const float* d_recs, int batch, const KParams& P, float* d_forces,
-                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
-                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(cmpc_solve_reg_kernel<2>, dim3(grid), dim3(128), 0, stream, d_recs, batch, P,
-                     d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
+                         uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
+                         int* ovf_list, int* ovf_count, int grid, hipStream_t stream) {
+  (void)batch;
+  hipLaunchKernelGGL(cmpc_solve_c2_kernel, dim3(grid), dim3(NV), 0, stream, d_recs, P, d_forces,
+                     d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
   return hipGetLastError();
 }
 

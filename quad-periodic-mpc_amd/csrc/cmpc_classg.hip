@@ -282,7 +282,7 @@ __device__ void solve_g(const float* __restrict__ rec, const KParams& P, SharedG
       const Cons cp = decode_cons(p, mui, sh.sub[p / 6]);
       float up = 0.f;
       for (;;) {
-        if (++iters > P.max_iter) { status = CMPC_MAX_ITER; break; }
+        if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
         // d = J' n+
         const float* Ja = J + (size_t)cp.ia * ld;
         const float* Jz = J + (size_t)cp.iz * ld;

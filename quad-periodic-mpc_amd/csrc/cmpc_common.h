@@ -22,35 +22,100 @@ constexpr int MAXN = CMPC_MAX_HORIZON;
 constexpr float kBigF = 3.0e38f;
 
 // ---------------------------------------------------------------------------------------------
-// wavefront helpers
+// wavefront helpers. Reductions use DPP lane permutes inside the VALU (row permutes, then the
+// row_bcast15 / row_bcast31 steps across the four 16-lane rows) and hand back a wave-uniform
+// result through v_readlane: no ds_bpermute round trips through the LDS crossbar and no
+// per-lane shuffle addresses for the optimiser to hoist out of loops.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float rl(float x, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
+}
+__device__ __forceinline__ int rli(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
+
+// DPP16 controls (GFX9 encoding)
+constexpr int kDppQuadSwap1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int kDppQuadSwap2 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int kDppRowShl = 0x100;     // + n: lane i <- lane i + n of the same row
+constexpr int kDppRowShr = 0x110;     // + n: lane i <- lane i - n of the same row
+constexpr int kDppWaveShl1 = 0x130;   // lane i <- lane i + 1
+constexpr int kDppWaveShr1 = 0x138;   // lane i <- lane i - 1
+constexpr int kDppRowMirror = 0x140;
+constexpr int kDppRowHalfMirror = 0x141;
+constexpr int kDppRowBcast15 = 0x142;
+constexpr int kDppRowBcast31 = 0x143;
+
+// lanes whose source is outside the row/wave, or whose row is masked off, get `old`
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dppf(float old, float src) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL, ROW_MASK, 0xf, false));
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ int dppi(int old, int src) {
+  return __builtin_amdgcn_update_dpp(old, src, CTRL, ROW_MASK, 0xf, false);
+}
+
+// sum over the 64 lanes (uniform result)
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  v += dppf<kDppQuadSwap1>(0.f, v);
+  v += dppf<kDppQuadSwap2>(0.f, v);
+  v += dppf<kDppRowHalfMirror>(0.f, v);
+  v += dppf<kDppRowMirror>(0.f, v);
+  v += dppf<kDppRowBcast15, 0xa>(0.f, v);
+  v += dppf<kDppRowBcast31, 0xc>(0.f, v);
+  return rl(v, 63);
 }
+// max over the 64 lanes (uniform result)
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
+  constexpr float ninf = -__builtin_huge_valf();
+  v = fmaxf(v, dppf<kDppQuadSwap1>(ninf, v));
+  v = fmaxf(v, dppf<kDppQuadSwap2>(ninf, v));
+  v = fmaxf(v, dppf<kDppRowHalfMirror>(ninf, v));
+  v = fmaxf(v, dppf<kDppRowMirror>(ninf, v));
+  v = fmaxf(v, dppf<kDppRowBcast15, 0xa>(ninf, v));
+  v = fmaxf(v, dppf<kDppRowBcast31, 0xc>(ninf, v));
+  return rl(v, 63);
 }
-// argmin with a deterministic tie-break on the smaller index
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ void argmin_step(float& v, int& i) {
+  const float ov = dppf<CTRL, ROW_MASK>(__builtin_huge_valf(), v);
+  const int oi = dppi<CTRL, ROW_MASK>(0x7fffffff, i);
+  if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+}
+// lexicographic (value, index) minimum over the 64 lanes, i.e. argmin with a deterministic
+// tie-break on the smaller index (uniform result)
 __device__ __forceinline__ void wave_argmin(float& v, int& i) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const float ov = __shfl_xor(v, off, 64);
-    const int oi = __shfl_xor(i, off, 64);
-    if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
-  }
+  argmin_step<kDppQuadSwap1>(v, i);
+  argmin_step<kDppQuadSwap2>(v, i);
+  argmin_step<kDppRowHalfMirror>(v, i);
+  argmin_step<kDppRowMirror>(v, i);
+  argmin_step<kDppRowBcast15, 0xa>(v, i);
+  argmin_step<kDppRowBcast31, 0xc>(v, i);
+  v = rl(v, 63);
+  i = rli(i, 63);
 }
-// inclusive suffix sum over lanes: s_l = sum_{m >= l} v_m
+// inclusive suffix sum over lanes: s_l = sum_{m >= l} v_m (a true suffix scan, no
+// total-minus-prefix cancellation): row-local scan with row_shl, then the later rows' totals
 __device__ __forceinline__ float wave_suffix_sum(float v, int lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float t = __shfl_down(v, off, 64);
-    if (lane + off < 64) v += t;
-  }
-  return v;
+  v += dppf<kDppRowShl + 1>(0.f, v);
+  v += dppf<kDppRowShl + 2>(0.f, v);
+  v += dppf<kDppRowShl + 4>(0.f, v);
+  v += dppf<kDppRowShl + 8>(0.f, v);
+  const float r1 = rl(v, 16), r2 = rl(v, 32), r3 = rl(v, 48);
+  const int row = lane >> 4;
+  return v + ((row == 0) ? r1 + (r2 + r3) : (row == 1) ? r2 + r3 : (row == 2) ? r3 : 0.f);
+}
+// value of lane l - 1 (lane 0 gets `old`) / lane l + 1 (lane 63 gets `old`)
+__device__ __forceinline__ float lane_prev(float old, float v) { return dppf<kDppWaveShr1>(old, v); }
+__device__ __forceinline__ float lane_next(float old, float v) { return dppf<kDppWaveShl1>(old, v); }
+__device__ __forceinline__ int lane_next_i(int old, int v) { return dppi<kDppWaveShl1>(old, v); }
+
+// thread index the optimiser cannot treat as loop-invariant: per-lane addresses derived from it
+// are recomputed where they are used instead of being hoisted out of long loops (and spilled)
+__device__ __forceinline__ int tid_opq() {
+  int x = threadIdx.x;
+  asm volatile("" : "+v"(x));
+  return x;
 }
 
 template <int I, int E, class F>
@@ -60,11 +125,6 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for<I + 1, E>(f);
   }
 }
-
-__device__ __forceinline__ float rl(float x, int lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), lane));
-}
-__device__ __forceinline__ int rli(int x, int lane) { return __builtin_amdgcn_readlane(x, lane); }
 // An SGPR value the compiler cannot see through: keeps per-iteration scalar work of an unrolled
 // loop inside its iteration (otherwise LICM hoists dozens of SGPRs out of it -> spills).
 __device__ __forceinline__ int opaque(int x) {

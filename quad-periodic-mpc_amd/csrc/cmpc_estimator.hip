@@ -1,0 +1,258 @@
+// cmpc_estimator.hip — config 5: the periodic-disturbance estimator of solve_mpc, batched.
+//
+// Per instance and per MPC step, what the reference does in globals of SolverMPC.cpp before it
+// condenses (SolverMPC.cpp:688-811), preceded by the caller's residual when LogData records are
+// given (ConvexMPCLocomotion.cpp:639-771):
+//   f_ext = x_k - A_prev x_prev - B_prev u_prev  (continuous model of the logged step, no dt)
+//   push (f_ext[3], simulation_time); while 400 <= count <= 500:
+//     band = gaussian_filter(window, 7) - gaussian_filter(window, 27)   (SolverMPC.cpp:404-437)
+//     fit_sin: peak |rfft| bin >= 1, amp = sqrt(2) std, offset = mean   (SolverMPC.cpp:478-541)
+//   count >= 400: f_est(3) = est_amp + sin(2 pi t est_freq + est_phase)  (sic '+', :766)
+//   qg uses f_est only when count > 500 (:808) -> record flag bit 0.
+//
+// MI355X mapping: one 256-thread workgroup per instance. The 400-sample window is staged in LDS
+// as double; each thread produces output samples of both Gaussian FIRs (43 and 163 taps, float
+// taps computed on the host exactly as the reference computes them, accumulated in double), then
+// one DFT bin (k = 1..200) each against a 400-entry twiddle table in LDS; the peak, mean and std
+// are workgroup reductions. Instances outside the estimation window only push their sample
+// (a few words of HBM traffic) and evaluate the compensation.
+#include "cmpc_common.h"
+
+namespace cmpc {
+namespace {
+
+constexpr int W = CMPC_EST_WINDOW;
+constexpr int NT = 256;
+constexpr int NWV = NT / 64;
+constexpr int NBIN = W / 2;  // bins 1..200 are searched (bin 0 excluded, SolverMPC.cpp:503-510)
+
+struct SharedE {
+  double d[W];       // window, oldest first
+  double band[W];    // blur7 - blur27
+  double twc[W], tws[W];
+  double redd[NWV];
+  float redv[NWV];
+  int redi[NWV];
+  float k7[2 * kGaussR7 + 1], k27[2 * kGaussR27 + 1];
+  int count, head;
+  float t_now, t0, t1;
+};
+
+__device__ __forceinline__ double block_sum_d(double x, SharedE& sh) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh.redd[wv] = x;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < NWV; i++) s += sh.redd[i];
+  __syncthreads();
+  return s;
+}
+
+// residual of ConvexMPCLocomotion.cpp:639-771 for one instance (one thread)
+__device__ void residual(const float* __restrict__ lg, const float* __restrict__ rec, float f_ext[6]) {
+  const float* R = lg + CMPC_LOG_ROT;  // R_yaw of the logged step, row-major
+  const float Ib[3] = {0.07f, 0.26f, 0.242f};
+  float Iw[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      Iw[i * 3 + j] = R[i * 3 + 0] * Ib[0] * R[j * 3 + 0] + R[i * 3 + 1] * Ib[1] * R[j * 3 + 1] +
+                      R[i * 3 + 2] * Ib[2] * R[j * 3 + 2];
+  const float c00 = Iw[4] * Iw[8] - Iw[5] * Iw[7];
+  const float c10 = Iw[5] * Iw[6] - Iw[3] * Iw[8];
+  const float c20 = Iw[3] * Iw[7] - Iw[4] * Iw[6];
+  const float idet = 1.f / (Iw[0] * c00 + Iw[1] * c10 + Iw[2] * c20);
+  float Ii[9];
+  Ii[0] = c00 * idet; Ii[1] = (Iw[2] * Iw[7] - Iw[1] * Iw[8]) * idet; Ii[2] = (Iw[1] * Iw[5] - Iw[2] * Iw[4]) * idet;
+  Ii[3] = c10 * idet; Ii[4] = (Iw[0] * Iw[8] - Iw[2] * Iw[6]) * idet; Ii[5] = (Iw[2] * Iw[3] - Iw[0] * Iw[5]) * idet;
+  Ii[6] = c20 * idet; Ii[7] = (Iw[1] * Iw[6] - Iw[0] * Iw[7]) * idet; Ii[8] = (Iw[0] * Iw[4] - Iw[1] * Iw[3]) * idet;
+  // B_prev u_prev, u_prev = -logged forces: rows 6..8 sum_b I_inv [r_b]x u_b, rows 9..11 sum_b u_b / m
+  float tq[3] = {0.f, 0.f, 0.f}, fs[3] = {0.f, 0.f, 0.f};
+  for (int b = 0; b < 4; b++) {
+    const float r0 = lg[CMPC_LOG_R + 0 * 4 + b], r1 = lg[CMPC_LOG_R + 1 * 4 + b], r2 = lg[CMPC_LOG_R + 2 * 4 + b];
+    const float u0 = -lg[CMPC_LOG_FORCE + 3 * b + 0], u1 = -lg[CMPC_LOG_FORCE + 3 * b + 1],
+                u2 = -lg[CMPC_LOG_FORCE + 3 * b + 2];
+    const float cm[9] = {0.f, -r2, r1, r2, 0.f, -r0, -r1, r0, 0.f};
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      float m0 = 0.f, m1 = 0.f, m2 = 0.f;  // (I_inv cm)[i][:]
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        m0 += Ii[i * 3 + k] * cm[k * 3 + 0];
+        m1 += Ii[i * 3 + k] * cm[k * 3 + 1];
+        m2 += Ii[i * 3 + k] * cm[k * 3 + 2];
+      }
+      tq[i] += m0 * u0 + m1 * u1 + m2 * u2;
+    }
+    fs[0] += (1.f / 12.f) * u0;
+    fs[1] += (1.f / 12.f) * u1;
+    fs[2] += (1.f / 12.f) * u2;
+  }
+  // A_prev x_prev: rows 6..10 are zero; row 11 = x_drag * v_x + x(12)
+  const float ax11 = lg[CMPC_LOG_XDRAG] * lg[CMPC_LOG_LIN + 0] + (-9.81f);
+  const float e6 = rec[CMPC_REC_W + 0] - tq[0];
+  const float e7 = rec[CMPC_REC_W + 1] - tq[1];
+  const float e8 = rec[CMPC_REC_W + 2] - tq[2];
+  const float e9 = rec[CMPC_REC_V + 0] - fs[0];
+  const float e10 = rec[CMPC_REC_V + 1] - fs[1];
+  const float e11 = (rec[CMPC_REC_V + 2] - ax11) - fs[2];
+  f_ext[0] = -e6;
+  f_ext[1] = -e7;
+  f_ext[2] = e8;
+  f_ext[3] = e9;
+  f_ext[4] = e10;
+  f_ext[5] = e11;
+}
+
+__global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
+    float* __restrict__ est, const float* __restrict__ logs, const float* __restrict__ fext3,
+    const float* __restrict__ times, float sim_time, float* __restrict__ recs, int rec_words,
+    float* __restrict__ fext6, const float* __restrict__ gauss, int batch) {
+  __shared__ SharedE sh;
+  const int inst = blockIdx.x;
+  if (inst >= batch) return;
+  const int tid = threadIdx.x;
+  float* st = est + (size_t)inst * CMPC_EST_WORDS;
+  float* rec = recs + (size_t)inst * rec_words;
+  int32_t* sti = reinterpret_cast<int32_t*>(st);
+  if (tid == 0) {
+    float f3;
+    if (logs) {
+      float fe[6];
+      residual(logs + (size_t)inst * CMPC_LOG_WORDS, rec, fe);
+      f3 = fe[3];
+      if (fext6) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) fext6[(size_t)inst * 6 + i] = fe[i];
+      }
+    } else {
+      f3 = fext3[inst];
+    }
+    const float t = times ? times[inst] : sim_time;
+    int count = sti[CMPC_EST_COUNT];
+    int head = sti[CMPC_EST_HEAD];
+    st[CMPC_EST_F + head] = f3;  // diff_history.push_back(f_ext(3))
+    st[CMPC_EST_T + head] = t;   // time_history.push_back(simulation_time)
+    head = (head + 1) % W;
+    if (count < (1 << 30)) count++;
+    sti[CMPC_EST_COUNT] = count;
+    sti[CMPC_EST_HEAD] = head;
+    sh.count = count;
+    sh.head = head;
+    sh.t_now = t;
+  }
+  __syncthreads();
+  const int count = sh.count;
+  double* prm = reinterpret_cast<double*>(st + CMPC_EST_PARAMS);  // stat, amp, freq, phase
+  if (count >= W && count <= CMPC_EST_STOP) {
+    const int head = sh.head;
+    for (int i = tid; i < W; i += NT) {
+      const int idx = (head + i) % W;
+      sh.d[i] = (double)st[CMPC_EST_F + idx];
+      double sn, cs;
+      sincospi(2.0 * (double)i / (double)W, &sn, &cs);
+      sh.twc[i] = cs;
+      sh.tws[i] = sn;
+    }
+    for (int i = tid; i < 2 * kGaussR7 + 1; i += NT) sh.k7[i] = gauss[i];
+    for (int i = tid; i < 2 * kGaussR27 + 1; i += NT) sh.k27[i] = gauss[2 * kGaussR7 + 1 + i];
+    if (tid == 0) {
+      sh.t0 = st[CMPC_EST_T + head];
+      sh.t1 = st[CMPC_EST_T + (head + 1) % W];
+    }
+    __syncthreads();
+    // band-pass: gaussian_filter(7) - gaussian_filter(27), edge clamped, taps in ascending order
+    for (int i = tid; i < W; i += NT) {
+      double a7 = 0.0, a27 = 0.0;
+      for (int j = -kGaussR7; j <= kGaussR7; j++) {
+        const int idx = min(max(i + j, 0), W - 1);
+        a7 += sh.d[idx] * (double)sh.k7[j + kGaussR7];
+      }
+      for (int j = -kGaussR27; j <= kGaussR27; j++) {
+        const int idx = min(max(i + j, 0), W - 1);
+        a27 += sh.d[idx] * (double)sh.k27[j + kGaussR27];
+      }
+      sh.band[i] = a7 - a27;
+    }
+    __syncthreads();
+    // mean and standard deviation of the band (fit_sin's amplitude and offset guesses)
+    double part = 0.0;
+    for (int i = tid; i < W; i += NT) part += sh.band[i];
+    const double mean = block_sum_d(part, sh) / W;
+    part = 0.0;
+    for (int i = tid; i < W; i += NT) part += (sh.band[i] - mean) * (sh.band[i] - mean);
+    const double sd = sqrt(block_sum_d(part, sh) / W);
+    // |DFT| of bins 1..200 and the first maximum
+    float best = -1.f;
+    int bk = 0x7fffffff;
+    double bestd = -1.0;
+    if (tid < NBIN) {
+      const int k = tid + 1;
+      double re = 0.0, im = 0.0;
+      int m = 0;  // (k t) mod W
+      for (int t = 0; t < W; t++) {
+        re += sh.band[t] * sh.twc[m];
+        im -= sh.band[t] * sh.tws[m];
+        m += k;
+        if (m >= W) m -= W;
+      }
+      bestd = sqrt(re * re + im * im);
+      bk = k;
+    }
+    // argmax in double with ties to the smaller bin: reduce on (-mag, k)
+    {
+      double v = (tid < NBIN) ? -bestd : __builtin_huge_val();
+      int i = bk;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const double ov = __shfl_xor(v, off, 64);
+        const int oi = __shfl_xor(i, off, 64);
+        if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
+      }
+      const int wv = tid >> 6;
+      if ((tid & 63) == 0) { sh.redd[wv] = v; sh.redi[wv] = i; }
+      __syncthreads();
+      if (tid == 0) {
+        double bv = sh.redd[0];
+        int bi = sh.redi[0];
+        for (int w = 1; w < NWV; w++)
+          if (sh.redd[w] < bv || (sh.redd[w] == bv && sh.redi[w] < bi)) { bv = sh.redd[w]; bi = sh.redi[w]; }
+        const double dt = (double)sh.t1 - (double)sh.t0;
+        const double guess_freq = fabs(bi / (W * dt));  // fftfreq(n, dt)[k], k <= n/2
+        const double omega = 2 * M_PI * guess_freq;
+        prm[0] = mean;               // est_stat = offset
+        prm[1] = sd * sqrt(2.0);     // est_amp
+        prm[2] = omega / (2 * M_PI); // est_freq
+        prm[3] = 0.0;                // est_phase
+      }
+      (void)best;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    float f_est3 = st[CMPC_EST_FEST3];
+    if (count >= W) {
+      f_est3 = (float)(prm[1] + sin(2 * M_PI * (double)sh.t_now * prm[2] + prm[3]));
+      st[CMPC_EST_FEST3] = f_est3;
+    }
+    rec[CMPC_REC_FEST3] = f_est3;
+    reinterpret_cast<uint32_t*>(rec)[CMPC_REC_FLAGS] = (count > CMPC_EST_STOP) ? 1u : 0u;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_estimate(float* d_est, const float* d_logs, const float* d_fext3,
+                           const float* d_time, float sim_time, float* d_records, int rec_words,
+                           float* d_fext6, const float* d_gauss, int batch, hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cmpc_estimate_kernel, dim3(batch), dim3(NT), 0, stream, d_est, d_logs, d_fext3,
+                     d_time, sim_time, d_records, rec_words, d_fext6, d_gauss, batch);
+  return hipGetLastError();
+}
+
+}  // namespace cmpc

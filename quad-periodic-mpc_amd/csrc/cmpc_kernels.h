@@ -16,7 +16,7 @@ struct KParams {
   float wts[12];
   int N;
   int rec_words;
-  int max_iter;
+  int max_iter;    // active-set cap; the kernels allow max_iter + 2 n
   int pad;
 };
 
@@ -41,6 +41,15 @@ hipError_t launch_class2(const float* d_recs, int batch, const KParams& P, float
 hipError_t launch_classg(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          float* scratch, int grid, hipStream_t stream);
+// config 5 estimator (cmpc_estimator.hip). d_gauss: the two normalised float Gaussian kernels
+// of gaussian_filter (sigma 7: 43 taps, then sigma 27: 163 taps), built on the host exactly as
+// SolverMPC.cpp:404-418 builds them.
+constexpr int kGaussR7 = 21;   // ceil(3 * 7)
+constexpr int kGaussR27 = 81;  // ceil(3 * 27)
+constexpr int kGaussTaps = 2 * kGaussR7 + 1 + 2 * kGaussR27 + 1;
+hipError_t launch_estimate(float* d_est, const float* d_logs, const float* d_fext3,
+                           const float* d_time, float sim_time, float* d_records, int rec_words,
+                           float* d_fext6, const float* d_gauss, int batch, hipStream_t stream);
 // parity hook: full (nothing eliminated) qH [12N x 12N] / qg [12N] per instance
 hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
                            float* scratch, int grid, hipStream_t stream);

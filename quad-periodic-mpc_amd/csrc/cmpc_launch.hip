@@ -1,6 +1,6 @@
 // cmpc_launch.hip — orchestration of the size classes for one batch solve (host code).
 //   class 1 (cmpc_class1.hip): every instance, one wavefront each; n > 64  -> list 1
-//   class 2 (cmpc_class2.hip): persistent 128-lane workgroups over list 1; n > 128 -> list 2
+//   class 2 (cmpc_class2.hip): one 128-lane workgroup per list-1 entry; n > 128 -> list 2
 //   class G (cmpc_classg.hip): persistent 256-lane workgroups over list 2 (any n)
 #include "cmpc_kernels.h"
 
@@ -23,8 +23,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   if (e != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (12 * P.N > 64) {
-    const int g2 = batch < 2048 ? batch : 2048;
-    e = launch_class2(d_recs, batch, P, d_forces, d_status, d_iters, list1, cnt1, list2, cnt2, g2,
+    // one workgroup per possible list-1 entry; surplus workgroups exit after one load
+    e = launch_class2(d_recs, batch, P, d_forces, d_status, d_iters, list1, cnt1, list2, cnt2, batch,
                       stream);
     if (e != hipSuccess) return e;
   }

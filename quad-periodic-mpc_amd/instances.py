@@ -101,3 +101,48 @@ def make_instances(batch: int, horizon: int = 10, seed: int = BASE_SEED, dt: flo
     x_drag = g.uniform(-x_drag_range, x_drag_range, B)
     rpy = np.stack([roll, pitch, yaw], -1)
     return pack_records(p, v, q, w, r, traj.reshape(B, 12 * N), gait, rpy=rpy, x_drag=x_drag)
+
+
+def make_disturbance(batch: int, steps: int, seed: int = BASE_SEED + 5, dt: float = 0.026,
+                     d_s: float = -10.0, d_n: float = 15.0, freq: float = 0.33, noise: float = 1.0,
+                     t0: float = 0.0):
+    """Config-5 residual samples f_ext[3] for ``steps`` MPC steps of ``batch`` instances:
+    ``d_s + d_n sin(2 pi f t + phi) + N(0, noise^2)`` with a random phase per instance and
+    t_k = t0 + k dt (the disturbance of raisim_unitree_ros_driver.hpp:126-129).
+    Returns (f3 [batch, steps] float32, t [steps] float32)."""
+    g = np.random.Generator(np.random.Philox(seed))
+    t = (t0 + dt * np.arange(steps)).astype(np.float32)
+    phi = g.uniform(0, 2 * np.pi, batch)
+    f3 = d_s + d_n * np.sin(2 * np.pi * freq * t[None, :].astype(np.float64) + phi[:, None])
+    f3 = f3 + noise * g.normal(0, 1, (batch, steps))
+    return f3.astype(np.float32), t
+
+
+def make_logs(records: np.ndarray, seed: int = BASE_SEED + 6) -> np.ndarray:
+    """LogData records (include/cmpc_solver.h CMPC_LOG_*) of a previous step near each
+    instance's current state: perturbed pose / twist, stance-like foot forces, the body rotation
+    and foot offsets of that step (fields read by ConvexMPCLocomotion.cpp:639-771)."""
+    from .records import (LOG_ANG, LOG_EUL, LOG_FORCE, LOG_LIN, LOG_POS, LOG_R, LOG_ROT,
+                          LOG_WORDS, LOG_XDRAG, REC_P, REC_R, REC_RPY, REC_V, REC_W, REC_XDRAG)
+    g = np.random.Generator(np.random.Philox(seed))
+    B = records.shape[0]
+    lg = np.zeros((B, LOG_WORDS), np.float32)
+    lg[:, LOG_POS:LOG_POS + 3] = records[:, REC_P:REC_P + 3] + g.normal(0, 0.01, (B, 3))
+    eul = records[:, REC_RPY:REC_RPY + 3] + g.normal(0, 0.01, (B, 3))
+    lg[:, LOG_EUL:LOG_EUL + 3] = eul
+    lg[:, LOG_ANG:LOG_ANG + 3] = records[:, REC_W:REC_W + 3] + g.normal(0, 0.05, (B, 3))
+    lg[:, LOG_LIN:LOG_LIN + 3] = records[:, REC_V:REC_V + 3] + g.normal(0, 0.05, (B, 3))
+    f = np.zeros((B, 4, 3))
+    f[:, :, 2] = g.uniform(20, 80, (B, 4))
+    f[:, :, :2] = g.normal(0, 5, (B, 4, 2))
+    lg[:, LOG_FORCE:LOG_FORCE + 12] = f.reshape(B, 12)
+    lg[:, LOG_XDRAG] = records[:, REC_XDRAG]
+    lg[:, LOG_R:LOG_R + 12] = records[:, REC_R:REC_R + 12]
+    q = euler_zyx_to_quat(eul[:, 0].astype(np.float64), eul[:, 1].astype(np.float64),
+                          eul[:, 2].astype(np.float64))
+    w, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R = np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                  2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                  2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], -1)
+    lg[:, LOG_ROT:LOG_ROT + 9] = R
+    return lg

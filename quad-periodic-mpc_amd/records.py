@@ -22,6 +22,13 @@ REC_FEST3 = 29   # f_est(3) compensation force (config 5)
 REC_FLAGS = 30   # uint32 bit-cast; bit 0: use f_est in qg
 REC_HDR = 32
 MAX_HORIZON = 24
+# config 5 (include/cmpc_solver.h CMPC_LOG_* / CMPC_EST_*)
+LOG_POS, LOG_EUL, LOG_ANG, LOG_LIN, LOG_FORCE, LOG_XDRAG, LOG_R, LOG_ROT = 0, 3, 6, 9, 12, 24, 25, 37
+LOG_WORDS = 48
+EST_WINDOW = 400
+EST_STOP = 500
+EST_F, EST_T, EST_COUNT, EST_HEAD, EST_FEST3, EST_PARAMS = 0, 400, 800, 801, 802, 804
+EST_WORDS = 816
 
 STATUS_NAMES = {0: "ok", 1: "max_iter", 2: "infeasible", 3: "not_pd", 4: "bad_input"}
 

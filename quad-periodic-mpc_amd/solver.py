@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "update_problem_data_floats", "_Z13update_x_dragf", "f_ext", "simulation_time",
     "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
     "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
-    "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing",
+    "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing", "cmpc_batch_estimate",
 )
 
 _lib = None
@@ -80,6 +80,9 @@ def load_library(path: str = LIB_PATH):
     lib.cmpc_last_error.restype = ctypes.c_char_p
     lib.cmpc_batch_enable_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.cmpc_batch_read_timing.argtypes = [ctypes.c_void_p, _fp, _ip, _ip]
+    lib.cmpc_batch_estimate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     _lib = lib
     return lib
 
@@ -225,6 +228,19 @@ class BatchSolver:
             batch = records.shape[0]
         _check(self.lib.cmpc_batch_condense(self._h, _ptr(records), int(batch), _ptr(H), _ptr(g)),
                "cmpc_batch_condense")
+
+    def estimate(self, est_state, records, *, logs=None, fext3=None, times=None,
+                 sim_time: float = 0.0, fext6=None, batch: int | None = None) -> None:
+        """Config-5 estimator step on device (``cmpc_batch_estimate``): updates ``est_state``
+        [B, EST_WORDS] and writes f_est(3) / the use-f_est flag into ``records``. Pass either
+        ``logs`` [B, LOG_WORDS] (residual computed on device) or ``fext3`` [B]."""
+        if batch is None:
+            batch = records.shape[0]
+        if logs is None and fext3 is None:
+            raise CmpcError("estimate needs logs or fext3")
+        _check(self.lib.cmpc_batch_estimate(self._h, _ptr(est_state), _ptr(logs), _ptr(fext3),
+                                            _ptr(times), float(sim_time), _ptr(records),
+                                            _ptr(fext6), int(batch)), "cmpc_batch_estimate")
 
     def enable_timing(self, steps: int) -> None:
         """Record HIP events around each size-class launch of the next ``steps`` solves."""

@@ -1,0 +1,59 @@
+"""Per-size-class diagnostics on the GPU: reduced sizes, active-set iterations and launch times of
+the bench workload, and the same launches with the active-set phase capped (max_iter), which
+splits each class's time into condensation + factorisation vs the QP iterations.
+
+  python scripts/diag_classes.py [--batch 65536 --horizon 10]
+"""
+import argparse
+import importlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--horizon", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+    cm = importlib.import_module("quad-periodic-mpc_amd")
+    sm = importlib.import_module("quad-periodic-mpc_amd.solver")
+    N, B = a.horizon, a.batch
+    recs_np = cm.make_instances(B, N, seed=20251015)
+    gait = cm.unpack_gait(recs_np, N)
+    n = 3 * (gait != 0).sum(1)
+    recs = torch.from_numpy(recs_np).cuda()
+    f = torch.empty((B, 12 * N), device="cuda")
+    st = torch.empty(B, dtype=torch.uint8, device="cuda")
+    it = torch.empty(B, dtype=torch.int32, device="cuda")
+    for cap in (100, 1, 0):
+        prm = cm.make_params(N, max_iter=cap)
+        s = sm.BatchSolver(prm, max_batch=B)
+        s.solve(recs, f, st, it)
+        torch.cuda.synchronize()
+        s.enable_timing(a.reps)
+        for _ in range(a.reps):
+            s.solve(recs, f, st, it)
+        ms, ovf = s.read_timing()
+        itn = it.cpu().numpy()
+        stn = st.cpu().numpy()
+        print(f"max_iter={cap}: class1 {ms[:, 0].mean():.3f} ms, class2+ {ms[:, 1].mean():.3f} ms, "
+              f"overflow {ovf}, status {np.bincount(stn, minlength=5).tolist()}", flush=True)
+        if cap == 100:
+            for lo, hi in ((0, 64), (65, 128), (129, 10000)):
+                m = (n >= lo) & (n <= hi)
+                if m.any():
+                    print(f"  n in [{lo},{hi}]: {m.sum()} instances, mean n {n[m].mean():.1f}, "
+                          f"iters mean {itn[m].mean():.2f} p50 {np.median(itn[m]):.0f} "
+                          f"p99 {np.percentile(itn[m], 99):.0f} max {itn[m].max()}", flush=True)
+        s.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -80,5 +80,36 @@ def main():
     build_set("n12_allstance", allstance_records(12, 4), cm.make_params(12), cond_count=1)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def build_config5_set(name="n20_config5", batch=32, steps=520, N=20):
+    """Config 5: the estimator sequence of every instance (oracle/cmpc_oracle.c restatement of
+    SolverMPC.cpp:404-553, 688-798, DFT pinned against numpy's FFT in tests/test_oracle.py),
+    then the final step's solve by the reference pipeline with f_est in qg (count > 500)."""
+    prm = cm.make_params(N)
+    recs = cm.make_instances(batch, N, seed=1008, random_contact_frac=0.0)
+    f3, t = cm.make_disturbance(batch, steps, seed=1009)
+    fest = np.zeros((batch, steps), np.float32)
+    flag = np.zeros((batch, steps), bool)
+    for i in range(batch):
+        st = np.zeros(orc.EST_WORDS, np.float32)
+        for k in range(steps):
+            fest[i, k], flag[i, k] = orc.est_step(st, f3[i, k], t[k])
+    final = recs.copy()
+    final[:, cm.records.REC_FEST3] = fest[:, -1]
+    final[:, cm.records.REC_FLAGS] = flag[:, -1].astype(np.uint32).view(np.float32)
+    q, status, nw = orc.ref_solve_batch(final, prm, nthreads=8)
+    logs = cm.make_logs(recs)
+    fext6 = np.stack([orc.residual(logs[i], recs[i]) for i in range(batch)])
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), records=recs, f3=f3, t=t, fest_ref=fest,
+                        flag_ref=flag, final_records=final, q_ref=q, status=status, nwsr=nw,
+                        logs=logs, fext6_ref=fext6, horizon=N, dt=prm.dt, mu=prm.mu,
+                        f_max=prm.f_max, weights=np.array(prm.weights, np.float32),
+                        alpha=prm.alpha)
+    print(name, "status", np.bincount(status), "f_est3 range", fest[:, -1].min(), fest[:, -1].max())
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "config5":
+    build_config5_set()

@@ -113,3 +113,95 @@ def test_golden_solutions_satisfy_kkt(cm):
         assert (fz >= -tol).all()
         assert (np.abs(fx) <= mu * fz + tol).all() and (np.abs(fy) <= mu * fz + tol).all()
         assert (fz <= float(g["f_max"]) + tol).all()
+
+
+# ---- config 5: periodic-disturbance estimation (parity anchor: numpy, since FFTW is absent) --
+def _np_gaussian(data, sigma):
+    """Independent numpy restatement of gaussian_filter (SolverMPC.cpp:404-437)."""
+    r = int(np.ceil(3 * sigma))
+    i = np.arange(-r, r + 1)
+    k = np.exp(-0.5 * (i * i) / np.float64(np.float32(sigma) * np.float32(sigma))).astype(np.float32)
+    s = np.float32(0)
+    for x in k:
+        s = np.float32(s + x)
+    k = (k / s).astype(np.float32)
+    idx = np.clip(np.arange(data.size)[:, None] + i[None, :], 0, data.size - 1)
+    return (data[idx] * k.astype(np.float64)[None, :]).sum(1)
+
+
+def test_gaussian_filter_matches_numpy(orc):
+    rng = np.random.default_rng(5)
+    x = rng.normal(0, 3, 400)
+    for sigma in (7.0, 27.0):
+        np.testing.assert_allclose(orc.gaussian_filter(x, sigma), _np_gaussian(x, sigma),
+                                   rtol=1e-12, atol=1e-12)
+
+
+def test_fit_sin_peak_matches_numpy_fft(cm, orc):
+    """The DFT-peak search (FFTW r2c in the reference, SolverMPC.cpp:489-510) against numpy's
+    FFT on band-passed config-5 windows: same peak bin, same frequency, amp = sqrt(2) std."""
+    f3, t = cm.make_disturbance(24, 400, seed=77)
+    for i in range(f3.shape[0]):
+        d = f3[i].astype(np.float64)
+        band = orc.gaussian_filter(d, 7.0) - orc.gaussian_filter(d, 27.0)
+        amp, freq, phase, offset, k = orc.fit_sin(t.astype(np.float64), band)
+        mags = np.abs(np.fft.rfft(band))
+        assert k == 1 + int(np.argmax(mags[1:]))
+        dt = float(t[1]) - float(t[0])
+        assert freq == pytest.approx(k / (400 * dt), rel=1e-12)
+        assert amp == pytest.approx(np.sqrt(2) * band.std(), rel=1e-10)
+        assert offset == pytest.approx(band.mean(), abs=1e-10)
+        assert phase == 0.0
+        assert abs(freq - 0.33) < 1.0 / (400 * dt)  # the injected 0.33 Hz disturbance
+
+
+def test_estimator_step_semantics(cm, orc):
+    """SolverMPC.cpp:688-811: no compensation before 400 samples, re-estimation while the
+    history holds 400..500 samples, f_est in qg only above 500, frozen estimate afterwards."""
+    f3, t = cm.make_disturbance(1, 560, seed=78)
+    st = np.zeros(orc.EST_WORDS, np.float32)
+    out = [orc.est_step(st, f3[0, k], t[k]) for k in range(560)]
+    fest = np.array([o[0] for o in out])
+    use = np.array([o[1] for o in out])
+    assert (fest[:399] == 0).all() and fest[399] != 0
+    assert not use[:500].any() and use[500:].all()
+    prm = st[804:812].view(np.float64)
+    amp, freq = prm[1], prm[2]
+    # after 500 samples the estimate is frozen: f_est3 = amp + sin(2 pi t f)
+    k = 555
+    assert fest[k] == np.float32(amp + np.sin(2 * np.pi * np.float64(t[k]) * freq))
+
+
+def test_residual_matches_numpy(cm, orc):
+    """ConvexMPCLocomotion.cpp:639-771 restated independently in numpy."""
+    recs = cm.make_instances(8, 10, seed=79)
+    logs = cm.make_logs(recs)
+    r = cm.records
+    for i in range(8):
+        lg, rec = logs[i].astype(np.float64), recs[i].astype(np.float64)
+        R = lg[r.LOG_ROT:r.LOG_ROT + 9].reshape(3, 3)
+        A = np.zeros((13, 13)); A[3, 9] = A[4, 10] = A[5, 11] = A[11, 12] = 1
+        A[11, 9] = lg[r.LOG_XDRAG]; A[0:3, 6:9] = R.T
+        Iinv = np.linalg.inv(R @ np.diag([0.07, 0.26, 0.242]) @ R.T)
+        B = np.zeros((13, 12))
+        for b in range(4):
+            rv = lg[r.LOG_R + np.array([0, 4, 8]) + b]
+            cmx = np.array([[0, -rv[2], rv[1]], [rv[2], 0, -rv[0]], [-rv[1], rv[0], 0]])
+            B[6:9, 3 * b:3 * b + 3] = Iinv @ cmx
+            B[9:12, 3 * b:3 * b + 3] = np.eye(3) / 12
+        xk = np.concatenate([rec[r.REC_RPY:r.REC_RPY + 3], rec[r.REC_P:r.REC_P + 3],
+                             rec[r.REC_W:r.REC_W + 3], rec[r.REC_V:r.REC_V + 3], [-9.81]])
+        xp = np.concatenate([lg[r.LOG_EUL:r.LOG_EUL + 3], lg[r.LOG_POS:r.LOG_POS + 3],
+                             lg[r.LOG_ANG:r.LOG_ANG + 3], lg[r.LOG_LIN:r.LOG_LIN + 3], [-9.81]])
+        e = xk - A @ xp - B @ (-lg[r.LOG_FORCE:r.LOG_FORCE + 12])
+        ref = np.array([-e[6], -e[7], e[8], e[9], e[10], e[11]])
+        np.testing.assert_allclose(orc.residual(logs[i], recs[i]), ref, rtol=2e-5, atol=2e-5)
+
+
+def test_config5_golden_self_consistent(cm, orc):
+    """The committed config-5 fixture replays through the oracle bit for bit."""
+    g = load_golden("n20_config5")
+    for i in range(4):
+        st = np.zeros(orc.EST_WORDS, np.float32)
+        seq = [orc.est_step(st, g["f3"][i, k], g["t"][k])[0] for k in range(g["f3"].shape[1])]
+        np.testing.assert_array_equal(np.array(seq, np.float32), g["fest_ref"][i])
