@@ -209,11 +209,11 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / FP32_PEAK_TFLOPS, 5) if achieved else None,
             "traffic": traffic,
-            "kernel": "cmpc_solve_kernel<1> (64-lane class)",
+            "kernel": "cmpc_solve_c1_kernel (64-lane class, one wavefront per instance)",
             "units_per_launch": int(units1),
             "flops_per_unit": fl,
             "avg_launch_ms": round(float(np.mean(c1)), 4),
-            "class2_avg_launch_ms": round(float(np.mean(c2)), 4),
+            "class2_avg_launch_ms": round(float(np.mean(c2)), 4),  # 128-lane class (+ class G)
             "class2_units_per_launch": int(ovf),
             "note": "FP32 compute roof (f32 VALU = f32 MFMA peak); algorithmic FLOPs per SURVEY "
                     "§8(d) F(N) (dense reference algorithm); HBM bytes/QP "

@@ -16,8 +16,9 @@
 //     symmetric, pivot column k is "register slot[k] of every lane": ONE ds_write_b32 per step
 //     publishes it, and the broadcast reads are ds_read_b128;
 //   * J = L^-T is built column-wise from the stored L columns (lane-local updates);
-//   * the QP's triangular factor R is implicit, R[i][j] = J[:,i]' n_j, since the pyramid
-//     normals n_j are 2-sparse (readlane of two J entries);
+//   * the QP's triangular factor R is explicit, packed upper columns in the LDS region that held
+//     L; its back substitution and re-triangularisation are readlane chains, and the J rows see
+//     only straight-line Givens chains (identity rotations outside the active range);
 //   * every loop over matrix columns is unrolled at compile time, so register indices are
 //     constants; LDS traffic between lanes of the single wavefront needs no s_barrier.
 // Everything is fp32 (the reference condenses in fp32: common_types.h:14).
@@ -40,6 +41,9 @@ __host__ __device__ constexpr int prow(int r) {
 }
 // prow(r) - (r & ~3): element (r, c) lives at prow0(r) + c
 __host__ __device__ constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+// R (upper triangular, q x q) packed by columns: R[i][j] at rcol(j) + i, i <= j
+__device__ __forceinline__ int rcol(int j) { return (j * (j + 1)) >> 1; }
+static_assert(NV * (NV + 1) / 2 <= PSZ, "R must fit in P");
 
 // prep scratch inside P (P is not yet holding H while these are live)
 constexpr int OFF_TRAJ = 0;
@@ -312,159 +316,201 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   lsync();
 
   // ---- Goldfarb-Idnani dual active set on the friction pyramids -----------------------------
+  // One flat loop, one active-set step per trip. The QP's triangular factor R (q x q) is kept
+  // explicitly, packed by columns in P (the L rows are dead once J is formed): back substitution
+  // and the re-triangularisation after a drop are readlane chains over LDS. The J rows in
+  // registers see the same straight-line code on every trip — a Householder reflection (the
+  // add step; beta = 0 on a drop) and an ascending Givens chain (the drop step; identity
+  // rotations otherwise) — so their registers carry through the loop without copies.
   const float mui = P.mu_inv;
   const float fnorm = rsqrtf(mui * mui + 1.f);
   int q = 0;
   int iters = 0;
   float u_reg = 0.f;   // lane j < q: dual of active constraint j
   int act_reg = 0;     // lane j < q: id of active constraint j
+  int p = -1;          // constraint being added (-1: pick the most violated one)
+  Cons cp{};
+  float up = 0.f;
+  lsync();
   if (status == CMPC_OK) {
     for (;;) {
-      sh.xs[v] = xv;
-      lsync();
-      float best = 0.f;
-      int bid = 0x7fffffff;
-      if (v < nfs) {
-        const float fx = sh.xs[3 * v], fy = sh.xs[3 * v + 1], fz = sh.xs[3 * v + 2];
-        float sl[6];
-        sl[0] = (mui * fx + fz) * fnorm;
-        sl[1] = (-mui * fx + fz) * fnorm;
-        sl[2] = (mui * fy + fz) * fnorm;
-        sl[3] = (-mui * fy + fz) * fnorm;
-        sl[4] = fz;
-        sl[5] = sh.sub[v] - fz;
+      pin(slot);
+      const int v = tid_opq();  // re-materialised: keeps per-lane addresses out of the preheader
+      if (p < 0) {
+        sh.xs[v] = xv;
+        lsync();
+        float best = 0.f;
+        int bid = 0x7fffffff;
+        if (v < nfs) {
+          const float fx = sh.xs[3 * v], fy = sh.xs[3 * v + 1], fz = sh.xs[3 * v + 2];
+          float sl[6];
+          sl[0] = (mui * fx + fz) * fnorm;
+          sl[1] = (-mui * fx + fz) * fnorm;
+          sl[2] = (mui * fy + fz) * fnorm;
+          sl[3] = (-mui * fy + fz) * fnorm;
+          sl[4] = fz;
+          sl[5] = sh.sub[v] - fz;
 #pragma unroll
-        for (int t = 0; t < 6; t++)
-          if (!sh.cflag[6 * v + t] && sl[t] < best) { best = sl[t]; bid = 6 * v + t; }
+          for (int t = 0; t < 6; t++)
+            if (!sh.cflag[6 * v + t] && sl[t] < best) { best = sl[t]; bid = 6 * v + t; }
+        }
+        const float xmax = wave_max(fabsf(xv));
+        wave_argmin(best, bid);
+        const float tol = 1e-5f * fmaxf(1.f, xmax);
+        if (bid == 0x7fffffff || best >= -tol) break;
+        p = __builtin_amdgcn_readfirstlane(bid);
+        cp = decode_cons(p, mui, sh.sub[p / 6]);
+        up = 0.f;
       }
-      const float xmax = wave_max(fabsf(xv));
-      wave_argmin(best, bid);
-      const float tol = 1e-5f * fmaxf(1.f, xmax);
-      if (bid == 0x7fffffff || best >= -tol) break;
-
-      const int p = __builtin_amdgcn_readfirstlane(bid);
-      const Cons cp = decode_cons(p, mui, sh.sub[p / 6]);
-      float up = 0.f;
-      for (;;) {
-        if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
-        pin(slot);
-        // d = J' n+ : rows ia, iz of J through LDS
-        if (v == cp.ia && cp.ia != cp.iz) {
+      if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
+      // d = J' n+ : rows ia, iz of J through LDS (dword stores: wide stores would tie the row
+      // registers into tuples)
+      if (v == cp.ia && cp.ia != cp.iz) {
 #pragma unroll
-          for (int c = 0; c < NV; c += 4)
-            *reinterpret_cast<float4*>(&sh.bufA[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
-        }
-        if (v == cp.iz) {
+        for (int c = 0; c < NV; c++) sh.bufA[c] = slot[c];
+      }
+      if (v == cp.iz) {
 #pragma unroll
-          for (int c = 0; c < NV; c += 4)
-            *reinterpret_cast<float4*>(&sh.bufB[c]) = make_float4(slot[c], slot[c + 1], slot[c + 2], slot[c + 3]);
+        for (int c = 0; c < NV; c++) sh.bufB[c] = slot[c];
+      }
+      lsync();
+      const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[v], cp.cb * sh.bufB[v]) : cp.cb * sh.bufB[v];
+      const float dm = (v >= q && v < n) ? dv : 0.f;
+      sh.vbuf[v] = dm;
+      lsync();
+      // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+, dn = |d|^2
+      float zv = 0.f, zn = 0.f;
+#pragma unroll
+      for (int c = 0; c < NV; c += 4) {
+        const float4 m4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+        zv = fmaf(slot[c + 0], m4.x, zv);
+        zv = fmaf(slot[c + 1], m4.y, zv);
+        zv = fmaf(slot[c + 2], m4.z, zv);
+        zv = fmaf(slot[c + 3], m4.w, zv);
+        zn += m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
+        CMPC_SWEEP_FENCE(c);
+      }
+      const float dn = wave_sum((v < n) ? dv * dv : 0.f);
+      // r = R^-1 d1: back substitution over the packed columns of R (lane i ends with r_i)
+      float acc = dv, r_reg = 0.f;
+      for (int i = q - 1; i >= 0; i--) {
+        const int off = rcol(i);
+        const float ri = fdiv(rl(acc, i), sh.P[off + i]);
+        if (v < i) acc = fmaf(-sh.P[off + v], ri, acc);
+        r_reg = (v == i) ? ri : r_reg;
+      }
+      // partial (dual) step t1, full (primal) step t2
+      float t1 = kBigF;
+      int kk = 0x7fffffff;
+      if (v < q && r_reg > 0.f) { t1 = fmaxf(fdiv(u_reg, r_reg), 0.f); kk = v; }
+      wave_argmin(t1, kk);
+      const float spv = fmaf(cp.ca, rl(xv, cp.ia), fmaf(cp.cb, rl(xv, cp.iz), -cp.bp));
+      const bool zero_step = !(zn > 1e-9f * dn);
+      const float t2 = zero_step ? kBigF : -fdiv(spv, zn);
+      const float t = fminf(t1, t2);
+      if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
+      if (v < q) u_reg = fmaf(-t, r_reg, u_reg);
+      up += t;
+      if (!zero_step) xv = fmaf(t, zv, xv);
+      const bool add = !zero_step && t2 <= t1;
+      float beta = 0.f;
+      if (add) {
+        // ---- add p: the Householder reflection I - beta w w' on columns q..n-1 maps
+        // d[q..n-1] to -sgn(d_q) |d[q..n-1]| e_q; R gains the column (d[0..q-1], -sgn ts)
+        const float ts = sqrtf(zn);
+        const float dq = rl(dv, q);
+        const float sgn = (dq >= 0.f) ? 1.f : -1.f;
+        beta = fast_rcp(ts * (ts + fabsf(dq)));  // 2 / (w'w)
+        sh.vbuf[v] = (v == q) ? dq + sgn * ts : dm;
+        *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(1.f, 0.f);
+        const int offq = rcol(q);
+        if (v < q) sh.P[offq + v] = dv;
+        if (v == q) {
+          sh.P[offq + q] = -sgn * ts;
+          u_reg = up;
+          act_reg = p;
         }
+        if (v == 0) sh.cflag[p] = 1;
+      } else {
+        // ---- drop active constraint kk: shift positions kk+1..q-1 down, remove column kk of
+        // R and re-triangularise rows kk..q-1 (lane c rebuilds column c of R in place: every
+        // read of an old entry precedes, in this wavefront's LDS order, the write reusing it)
+        sh.vbuf[v] = 0.f;
+        const int k = __builtin_amdgcn_readfirstlane(kk);
+        const int ak = rli(act_reg, k);
+        if (v == 0) sh.cflag[ak] = 0;
+        const int a_nx = lane_next_i(act_reg, act_reg);
+        const float u_nx = lane_next(u_reg, u_reg);
+        if (v >= k && v < q - 1) { act_reg = a_nx; u_reg = u_nx; }
+        if (v < k || v > q - 2) *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(1.f, 0.f);
+        const bool in_c = v >= k && v <= q - 2;
+        float top = in_c ? sh.P[rcol(v + 1) + k] : 0.f;
         lsync();
-        const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[v], cp.cb * sh.bufB[v]) : cp.cb * sh.bufB[v];
-        sh.vbuf[v] = (v >= q) ? dv : 0.f;
-        lsync();
-        // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+, dn = |d|^2
-        float zv = 0.f;
+        for (int r = 0; r < k; r++) {
+          const float x = in_c ? sh.P[rcol(v + 1) + r] : 0.f;
+          lsync();
+          if (in_c) sh.P[rcol(v) + r] = x;
+          lsync();
+        }
+        for (int j = k; j <= q - 2; j++) {
+          const bool on = in_c && v >= j;
+          const float bot = on ? sh.P[rcol(v + 1) + j + 1] : 0.f;
+          lsync();
+          const float a0 = rl(top, j), b0 = rl(bot, j);
+          const float h = sqrtf(a0 * a0 + b0 * b0);
+          float cc = 1.f, sn = 0.f;
+          if (h > 0.f) { const float ih = fast_rcp(h); cc = a0 * ih; sn = b0 * ih; }
+          if (on) {
+            sh.P[rcol(v) + j] = fmaf(cc, top, sn * bot);
+            top = fmaf(-sn, top, cc * bot);
+          }
+          if (v == 0) *reinterpret_cast<float2*>(&sh.cs[2 * j]) = make_float2(cc, sn);
+          lsync();
+        }
+      }
+      lsync();
+      // J <- J (I - beta w w'): tw = J_v . w, J_v -= beta tw w  (no-op on a drop: beta = 0)
+      {
+        float tw = 0.f;
 #pragma unroll
         for (int c = 0; c < NV; c += 4) {
-          const float4 m4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-          zv = fmaf(slot[c + 0], m4.x, zv);
-          zv = fmaf(slot[c + 1], m4.y, zv);
-          zv = fmaf(slot[c + 2], m4.z, zv);
-          zv = fmaf(slot[c + 3], m4.w, zv);
+          const float4 w4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+          tw = fmaf(slot[c + 0], w4.x, tw);
+          tw = fmaf(slot[c + 1], w4.y, tw);
+          tw = fmaf(slot[c + 2], w4.z, tw);
+          tw = fmaf(slot[c + 3], w4.w, tw);
           CMPC_SWEEP_FENCE(c);
         }
-        const float dsq = (v < n) ? dv * dv : 0.f;
-        const float dn = wave_sum(dsq);
-        const float zn = wave_sum((v >= q) ? dsq : 0.f);
-        // r = R^-1 d1, R[i][j] = J[:,i]' n_j: back substitution through m = sum_{j>i} r_j n_j
-        float m = 0.f, r_reg = 0.f;
-        static_for<0, NV>([&](auto IC) {
-          constexpr int i = NV - 1 - decltype(IC)::value;
-          if (i < q) {
-            const int ai = rli(act_reg, i);
-            const Cons ci = decode_cons(ai, mui, sh.sub[ai / 6]);
-            const float ja = rl(slot[i], ci.ia), jz = rl(slot[i], ci.iz);
-            const float Rii = fmaf(ci.ca, ja, ci.cb * jz);
-            const float sdot = wave_sum(slot[i] * m);
-            const float ri = fdiv(rl(dv, i) - sdot, Rii);
-            r_reg = (v == i) ? ri : r_reg;
-            if (v == ci.ia) m = fmaf(ci.ca, ri, m);
-            if (v == ci.iz) m = fmaf(ci.cb, ri, m);
-          }
-        });
-        // partial (dual) step t1, full (primal) step t2
-        float t1 = kBigF;
-        int kk = 0x7fffffff;
-        if (v < q && r_reg > 0.f) { t1 = fmaxf(fdiv(u_reg, r_reg), 0.f); kk = v; }
-        wave_argmin(t1, kk);
-        const float spv = fmaf(cp.ca, rl(xv, cp.ia), fmaf(cp.cb, rl(xv, cp.iz), -cp.bp));
-        const bool zero_step = !(zn > 1e-9f * dn);
-        const float t2 = zero_step ? kBigF : -fdiv(spv, zn);
-        const float t = fminf(t1, t2);
-        if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
-        if (v < q) u_reg = fmaf(-t, r_reg, u_reg);
-        up += t;
-        if (!zero_step) xv = fmaf(t, zv, xv);
-        if (!zero_step && t2 <= t1) {
-          // ---- add p: Givens rotations zeroing d[q+1..n-1] into d[q]; parameters in closed
-          // form from suffix norms ts_j = |d[j..n-1]|
-          const float ts = sqrtf(wave_suffix_sum((v >= q && v < n) ? dv * dv : 0.f, v));
-          const float ts_prev = lane_prev(ts, ts);
-          const float d_prev = lane_prev(dv, dv);
-          float cj = 1.f, sj = 0.f;
-          if (v > q && v < n && ts_prev > 0.f) {
-            const float ri = fast_rcp(ts_prev);
-            cj = d_prev * ri;
-            sj = ((v == n - 1) ? dv : ts) * ri;
-          }
-          *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(cj, sj);
-          lsync();
-          static_for<0, NV - 1>([&](auto IC) {
-            constexpr int j = NV - 1 - decltype(IC)::value;  // NV-1 .. 1
-            if ((unsigned)(j - q - 1) < (unsigned)(n - q - 1)) {  // q < j < n
-              const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
-              const float a0 = slot[j - 1], b0 = slot[j];
-              slot[j - 1] = fmaf(cs2.x, a0, cs2.y * b0);
-              slot[j] = fmaf(-cs2.y, a0, cs2.x * b0);
-            }
-          });
-          pin(slot);
-          if (v == q) { u_reg = up; act_reg = p; }
-          if (v == 0) sh.cflag[p] = 1;
-          q++;
-          lsync();
-          break;
-        }
-        // ---- drop active constraint kk, re-triangularise the implicit R -------------------
-        {
-          const int k = __builtin_amdgcn_readfirstlane(kk);
-          const int ak = rli(act_reg, k);
-          if (v == 0) sh.cflag[ak] = 0;
-          const int a_nx = lane_next_i(act_reg, act_reg);
-          const float u_nx = lane_next(u_reg, u_reg);
-          if (v >= k && v < q - 1) { act_reg = a_nx; u_reg = u_nx; }
-          static_for<0, NV - 1>([&](auto JC) {
-            constexpr int j = decltype(JC)::value;  // 0 .. NV-2
-            if ((unsigned)(j - k) < (unsigned)(q - 1 - k)) {  // k <= j < q-1
-              const int aj = rli(act_reg, j);
-              const Cons c2 = decode_cons(aj, mui, sh.sub[aj / 6]);
-              const float a0 = fmaf(c2.ca, rl(slot[j], c2.ia), c2.cb * rl(slot[j], c2.iz));
-              const float b0 = fmaf(c2.ca, rl(slot[j + 1], c2.ia), c2.cb * rl(slot[j + 1], c2.iz));
-              const float h = sqrtf(a0 * a0 + b0 * b0);
-              float c = 1.f, sn = 0.f;
-              if (h > 0.f) { const float ih = fast_rcp(h); c = a0 * ih; sn = b0 * ih; }
-              const float x0 = slot[j], x1 = slot[j + 1];
-              slot[j] = fmaf(c, x0, sn * x1);
-              slot[j + 1] = fmaf(-sn, x0, c * x1);
-            }
-          });
-          pin(slot);
-          q--;
-          lsync();
+        const float bt = -beta * tw;
+        // re-read w from LDS: without this point the compiler keeps all NV values of the first
+        // sweep's loads live for the second (a whole row of extra VGPRs)
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < NV; c += 4) {
+          const float4 w4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+          slot[c + 0] = fmaf(bt, w4.x, slot[c + 0]);
+          slot[c + 1] = fmaf(bt, w4.y, slot[c + 1]);
+          slot[c + 2] = fmaf(bt, w4.z, slot[c + 2]);
+          slot[c + 3] = fmaf(bt, w4.w, slot[c + 3]);
+          CMPC_SWEEP_FENCE(c);
         }
       }
-      if (status != CMPC_OK) break;
+      // J columns (j, j+1) <- Givens chain j = 0 .. NV-2 (identity on an add)
+      static_for<0, NV - 1>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+        const float x0 = slot[j], x1 = slot[j + 1];
+        slot[j] = fmaf(cs2.x, x0, cs2.y * x1);
+        slot[j + 1] = fmaf(-cs2.y, x0, cs2.x * x1);
+        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+      });
+      if (add) {
+        q++;
+        p = -1;
+      } else {
+        q--;
+      }
+      lsync();
     }
   }
 

@@ -89,7 +89,7 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
                                          int inst) {
   const int v = threadIdx.x;
   const int lane = v & 63;
-  const int wave = v >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(v >> 6);  // wave-uniform: scalar branches
   const int N = P.N;
   // ---- stance table + elimination (SolverMPC.cpp:869-894): both wavefronts compact it (same
   // result), wavefront 0 stores it
@@ -306,6 +306,10 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
   bar();  // L (in P) and y are dead from here; P holds R
 
   // ---- Goldfarb-Idnani dual active set on the friction pyramids -----------------------------
+  // One flat loop, one active-set step per trip (class 1's structure): the J rows see the same
+  // straight-line code on every trip (Householder reflection for an add, beta = 0 on a drop;
+  // ascending Givens chain for a drop, identity rotations on an add), so their registers carry
+  // through the loop without copies. R lives in P, maintained by wavefront 0.
   const float mui = P.mu_inv;
   const float fnorm = rsqrtf(mui * mui + 1.f);
   int q = 0;
@@ -313,239 +317,245 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
   // wavefront 0, lane l: active-set positions l and l + 64 (dual u, constraint id, dual step r)
   float u_lo = 0.f, u_hi = 0.f, r_lo = 0.f, r_hi = 0.f;
   int a_lo = 0, a_hi = 0;
+  int p = -1;          // constraint being added (-1: pick the most violated one)
+  Cons cp{};
+  float up = 0.f;
   if (status == CMPC_OK) {
     for (;;) {
-      // lane ids re-materialised per iteration (tid_opq): keeps per-lane LDS addresses out of
-      // the loop preheader, where they would be spilled
+      pin(slot);
+      // lane ids re-materialised per trip (tid_opq): keeps per-lane LDS addresses out of the
+      // loop preheader, where they would be spilled
       const int v = tid_opq();
       const int lane = v & 63;
+      if (p < 0) {
+        sh.xs[v] = xv;
+        {
+          const float wm = wave_max(fabsf(xv));
+          if (lane == 0) sh.redf[wave] = wm;
+        }
+        bar();
+        // most violated constraint (normalised slack): both wavefronts scan the same foot-steps
+        float best = 0.f;
+        int bid = kNone;
+        if (lane < nfs) {
+          const float fx = sh.xs[3 * lane], fy = sh.xs[3 * lane + 1], fz = sh.xs[3 * lane + 2];
+          float sl[6];
+          sl[0] = (mui * fx + fz) * fnorm;
+          sl[1] = (-mui * fx + fz) * fnorm;
+          sl[2] = (mui * fy + fz) * fnorm;
+          sl[3] = (-mui * fy + fz) * fnorm;
+          sl[4] = fz;
+          sl[5] = sh.sub[lane] - fz;
+#pragma unroll
+          for (int t = 0; t < 6; t++)
+            if (!sh.cflag[6 * lane + t] && sl[t] < best) { best = sl[t]; bid = 6 * lane + t; }
+        }
+        const float xmax = fmaxf(sh.redf[0], sh.redf[1]);
+        wave_argmin(best, bid);
+        const float tol = 1e-5f * fmaxf(1.f, xmax);
+        if (bid == kNone || best >= -tol) break;
+        p = __builtin_amdgcn_readfirstlane(bid);
+        cp = decode_cons(p, mui, sh.sub[p / 6]);
+        up = 0.f;
+      }
+      if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
+      // d = J' n+ : rows ia, iz of J through LDS (dword stores: 128-bit stores would tie the
+      // row registers into quads)
+      if (v == cp.ia && cp.ia != cp.iz) {
+#pragma unroll
+        for (int c = 0; c < NV; c++) sh.bufA[c] = slot[c];
+      }
+      if (v == cp.iz) {
+#pragma unroll
+        for (int c = 0; c < NV; c++) sh.bufB[c] = slot[c];
+      }
       sh.xs[v] = xv;
+      bar();
+      const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[v], cp.cb * sh.bufB[v]) : cp.cb * sh.bufB[v];
+      const float dm = (v >= q && v < n) ? dv : 0.f;
+      sh.vbuf[v] = dm;
+      sh.dfull[v] = dv;
       {
-        const float wm = wave_max(fabsf(xv));
-        if (lane == 0) sh.redf[wave] = wm;
+        const float dw = wave_sum((v < n) ? dv * dv : 0.f);
+        if (lane == 0) sh.redf[2 + wave] = dw;
+      }
+      const float spv = fmaf(cp.ca, sh.xs[cp.ia], fmaf(cp.cb, sh.xs[cp.iz], -cp.bp));
+      bar();
+      // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+, dn = |d|^2
+      float zv = 0.f, zn = 0.f;
+#pragma unroll
+      for (int c = 0; c < NV; c += 4) {
+        const float4 m4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+        zv = fmaf(slot[c + 0], m4.x, zv);
+        zv = fmaf(slot[c + 1], m4.y, zv);
+        zv = fmaf(slot[c + 2], m4.z, zv);
+        zv = fmaf(slot[c + 3], m4.w, zv);
+        zn += m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
+        CMPC_SWEEP_FENCE(c);
+      }
+      const float dn = sh.redf[2] + sh.redf[3];
+      // r = R^-1 d1 by back substitution over the packed columns of R (wavefront 0), then the
+      // partial (dual) step t1 = min_{r_j > 0} u_j / r_j
+      if (wave == 0) {
+        float acc_lo = dv;
+        float acc_hi = sh.dfull[lane + 64];
+        r_lo = 0.f;
+        r_hi = 0.f;
+        for (int i = q - 1; i >= 0; i--) {
+          const int off = rcol(i);
+          const float rii = sh.P[off + i];
+          const float ai = (i < 64) ? rl(acc_lo, i) : rl(acc_hi, i - 64);
+          const float ri = fdiv(ai, rii);
+          if (lane < i) acc_lo = fmaf(-sh.P[off + lane], ri, acc_lo);
+          if (lane + 64 < i) acc_hi = fmaf(-sh.P[off + lane + 64], ri, acc_hi);
+          r_lo = (lane == i) ? ri : r_lo;
+          r_hi = (lane + 64 == i) ? ri : r_hi;
+        }
+        float t1w = kBigF;
+        int kw = kNone;
+        if (lane < q && r_lo > 0.f) { t1w = fmaxf(fdiv(u_lo, r_lo), 0.f); kw = lane; }
+        if (lane + 64 < q && r_hi > 0.f) {
+          const float th = fmaxf(fdiv(u_hi, r_hi), 0.f);
+          if (th < t1w) { t1w = th; kw = lane + 64; }
+        }
+        wave_argmin(t1w, kw);
+        if (lane == 0) { sh.redf[4] = t1w; sh.redi[4] = kw; }
       }
       bar();
-      // most violated constraint (normalised slack): both wavefronts scan the same foot-steps
-      float best = 0.f;
-      int bid = kNone;
-      if (lane < nfs) {
-        const float fx = sh.xs[3 * lane], fy = sh.xs[3 * lane + 1], fz = sh.xs[3 * lane + 2];
-        float sl[6];
-        sl[0] = (mui * fx + fz) * fnorm;
-        sl[1] = (-mui * fx + fz) * fnorm;
-        sl[2] = (mui * fy + fz) * fnorm;
-        sl[3] = (-mui * fy + fz) * fnorm;
-        sl[4] = fz;
-        sl[5] = sh.sub[lane] - fz;
-#pragma unroll
-        for (int t = 0; t < 6; t++)
-          if (!sh.cflag[6 * lane + t] && sl[t] < best) { best = sl[t]; bid = 6 * lane + t; }
+      const float t1 = sh.redf[4];
+      const int kk = __builtin_amdgcn_readfirstlane(sh.redi[4]);
+      const bool zero_step = !(zn > 1e-9f * dn);
+      const float t2 = zero_step ? kBigF : -fdiv(spv, zn);
+      const float t = fminf(t1, t2);
+      if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
+      if (wave == 0) {
+        if (lane < q) u_lo = fmaf(-t, r_lo, u_lo);
+        if (lane + 64 < q) u_hi = fmaf(-t, r_hi, u_hi);
       }
-      const float xmax = fmaxf(sh.redf[0], sh.redf[1]);
-      wave_argmin(best, bid);
-      const float tol = 1e-5f * fmaxf(1.f, xmax);
-      if (bid == kNone || best >= -tol) break;
-
-      const int p = __builtin_amdgcn_readfirstlane(bid);
-      const Cons cp = decode_cons(p, mui, sh.sub[p / 6]);
-      float up = 0.f;
-      for (;;) {
-        if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
-        pin(slot);
-        const int v = tid_opq();
-        const int lane = v & 63;
-        // d = J' n+ : rows ia, iz of J through LDS
-        // (dword stores: 128-bit stores would tie slot[] into register quads and spill)
-        if (v == cp.ia && cp.ia != cp.iz) {
-#pragma unroll
-          for (int c = 0; c < NV; c++) sh.bufA[c] = slot[c];
+      up += t;
+      if (!zero_step) xv = fmaf(t, zv, xv);
+      const bool add = !zero_step && t2 <= t1;
+      float beta = 0.f;
+      if (add) {
+        // ---- add p: the Householder reflection I - beta w w' on columns q..n-1 maps
+        // d[q..n-1] to -sgn(d_q) |d[q..n-1]| e_q; R gains the column (d[0..q-1], -sgn ts)
+        const float ts = sqrtf(zn);
+        const float dq = sh.dfull[q];
+        const float sgn = (dq >= 0.f) ? 1.f : -1.f;
+        beta = fast_rcp(ts * (ts + fabsf(dq)));  // 2 / (w'w)
+        sh.vbuf[v] = (v == q) ? dq + sgn * ts : dm;
+        *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(1.f, 0.f);
+        const int offq = rcol(q);
+        if (v < q) sh.P[offq + v] = dv;
+        if (v == q) sh.P[offq + q] = -sgn * ts;
+        if (wave == 0) {
+          if (lane == q) { u_lo = up; a_lo = p; }
+          if (lane + 64 == q) { u_hi = up; a_hi = p; }
         }
-        if (v == cp.iz) {
-#pragma unroll
-          for (int c = 0; c < NV; c++) sh.bufB[c] = slot[c];
+        if (v == 0) sh.cflag[p] = 1;
+      } else {
+        // ---- drop active constraint kk: shift positions kk+1..q-1 down, remove column kk of
+        // R and re-triangularise rows kk..q-1 with Givens rotations (wavefront 0, in place)
+        sh.vbuf[v] = 0.f;
+        const int k = kk;
+        // identity rotations outside k <= j <= q-2 (wavefront 0 writes the others below)
+        if (v < k || v > q - 2) *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(1.f, 0.f);
+        if (wave == 0) {
+          const int ak = (k < 64) ? rli(a_lo, k) : rli(a_hi, k - 64);
+          if (lane == 0) sh.cflag[ak] = 0;
+          const int alo_nx = lane_next_i(a_lo, a_lo);
+          const float ulo_nx = lane_next(u_lo, u_lo);
+          const int ahi_nx = lane_next_i(a_hi, a_hi);
+          const float uhi_nx = lane_next(u_hi, u_hi);
+          const int ahi0 = rli(a_hi, 0);
+          const float uhi0 = rl(u_hi, 0);
+          if (lane >= k && lane < q - 1) {
+            a_lo = (lane == 63) ? ahi0 : alo_nx;
+            u_lo = (lane == 63) ? uhi0 : ulo_nx;
+          }
+          if (lane + 64 >= k && lane + 64 < q - 1) { a_hi = ahi_nx; u_hi = uhi_nx; }
+          // new column c (k <= c <= q-2) = old column c+1. Lane l handles c = l and l + 64.
+          // Every read of an old entry precedes, in this wavefront's LDS order, the write that
+          // reuses its word (new column c overlays old column c).
+          const int clo = lane, chi = lane + 64;
+          const bool in_lo = clo >= k && clo <= q - 2;
+          const bool in_hi = chi >= k && chi <= q - 2;
+          float top_lo = in_lo ? sh.P[rcol(clo + 1) + k] : 0.f;
+          float top_hi = in_hi ? sh.P[rcol(chi + 1) + k] : 0.f;
+          lsync();
+          for (int r = 0; r < k; r++) {
+            const float xlo = in_lo ? sh.P[rcol(clo + 1) + r] : 0.f;
+            const float xhi = in_hi ? sh.P[rcol(chi + 1) + r] : 0.f;
+            lsync();
+            if (in_lo) sh.P[rcol(clo) + r] = xlo;
+            if (in_hi) sh.P[rcol(chi) + r] = xhi;
+            lsync();
+          }
+          for (int j = k; j <= q - 2; j++) {
+            const bool on_lo = in_lo && clo >= j, on_hi = in_hi && chi >= j;
+            const float bot_lo = on_lo ? sh.P[rcol(clo + 1) + j + 1] : 0.f;
+            const float bot_hi = on_hi ? sh.P[rcol(chi + 1) + j + 1] : 0.f;
+            lsync();
+            const float a0 = (j < 64) ? rl(top_lo, j) : rl(top_hi, j - 64);
+            const float b0 = (j < 64) ? rl(bot_lo, j) : rl(bot_hi, j - 64);
+            const float h = sqrtf(a0 * a0 + b0 * b0);
+            float cc = 1.f, sn = 0.f;
+            if (h > 0.f) { const float ih = fast_rcp(h); cc = a0 * ih; sn = b0 * ih; }
+            if (on_lo) {
+              sh.P[rcol(clo) + j] = fmaf(cc, top_lo, sn * bot_lo);
+              top_lo = fmaf(-sn, top_lo, cc * bot_lo);
+            }
+            if (on_hi) {
+              sh.P[rcol(chi) + j] = fmaf(cc, top_hi, sn * bot_hi);
+              top_hi = fmaf(-sn, top_hi, cc * bot_hi);
+            }
+            if (lane == 0) *reinterpret_cast<float2*>(&sh.cs[2 * j]) = make_float2(cc, sn);
+            lsync();
+          }
         }
-        sh.xs[v] = xv;
-        bar();
-        const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[v], cp.cb * sh.bufB[v]) : cp.cb * sh.bufB[v];
-        const float dm = (v >= q && v < n) ? dv : 0.f;
-        sh.vbuf[v] = dm;
-        sh.dfull[v] = dv;
-        {
-          const float dw = wave_sum((v < n) ? dv * dv : 0.f);
-          if (lane == 0) sh.redf[2 + wave] = dw;
-        }
-        const float spv = fmaf(cp.ca, sh.xs[cp.ia], fmaf(cp.cb, sh.xs[cp.iz], -cp.bp));
-        bar();
-        // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+ (split at lane 64), dn = |d|^2
-        float zv = 0.f, zlo = 0.f, zhi = 0.f;
+      }
+      bar();
+      // J <- J (I - beta w w'): tw = J_v . w, J_v -= beta tw w  (no-op on a drop: beta = 0)
+      {
+        float tw = 0.f;
 #pragma unroll
         for (int c = 0; c < NV; c += 4) {
-          const float4 m4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-          zv = fmaf(slot[c + 0], m4.x, zv);
-          zv = fmaf(slot[c + 1], m4.y, zv);
-          zv = fmaf(slot[c + 2], m4.z, zv);
-          zv = fmaf(slot[c + 3], m4.w, zv);
-          const float s4 = m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
-          if (c < 64) zlo += s4; else zhi += s4;
+          const float4 w4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+          tw = fmaf(slot[c + 0], w4.x, tw);
+          tw = fmaf(slot[c + 1], w4.y, tw);
+          tw = fmaf(slot[c + 2], w4.z, tw);
+          tw = fmaf(slot[c + 3], w4.w, tw);
           CMPC_SWEEP_FENCE(c);
         }
-        const float zn = zlo + zhi;
-        const float dn = sh.redf[2] + sh.redf[3];
-        // r = R^-1 d1 by back substitution over the packed columns of R (wavefront 0), then the
-        // partial (dual) step t1 = min_{r_j > 0} u_j / r_j
-        if (wave == 0) {
-          float acc_lo = dv;
-          float acc_hi = sh.dfull[lane + 64];
-          for (int i = q - 1; i >= 0; i--) {
-            const int off = rcol(i);
-            const float rii = sh.P[off + i];
-            const float ai = (i < 64) ? rl(acc_lo, i) : rl(acc_hi, i - 64);
-            const float ri = fdiv(ai, rii);
-            if (lane < i) acc_lo = fmaf(-sh.P[off + lane], ri, acc_lo);
-            if (lane + 64 < i) acc_hi = fmaf(-sh.P[off + lane + 64], ri, acc_hi);
-            r_lo = (lane == i) ? ri : r_lo;
-            r_hi = (lane + 64 == i) ? ri : r_hi;
-          }
-          float t1w = kBigF;
-          int kw = kNone;
-          if (lane < q && r_lo > 0.f) { t1w = fmaxf(fdiv(u_lo, r_lo), 0.f); kw = lane; }
-          if (lane + 64 < q && r_hi > 0.f) {
-            const float th = fmaxf(fdiv(u_hi, r_hi), 0.f);
-            if (th < t1w) { t1w = th; kw = lane + 64; }
-          }
-          wave_argmin(t1w, kw);
-          if (lane == 0) { sh.redf[4] = t1w; sh.redi[4] = kw; }
-        }
-        bar();
-        const float t1 = sh.redf[4];
-        const int kk = __builtin_amdgcn_readfirstlane(sh.redi[4]);
-        const bool zero_step = !(zn > 1e-9f * dn);
-        const float t2 = zero_step ? kBigF : -fdiv(spv, zn);
-        const float t = fminf(t1, t2);
-        if (t >= kBigF) { status = CMPC_INFEASIBLE; break; }
-        if (wave == 0) {
-          if (lane < q) u_lo = fmaf(-t, r_lo, u_lo);
-          if (lane + 64 < q) u_hi = fmaf(-t, r_hi, u_hi);
-        }
-        up += t;
-        if (!zero_step) xv = fmaf(t, zv, xv);
-        if (!zero_step && t2 <= t1) {
-          // ---- add p: Givens rotations zeroing d[q+1..n-1] into d[q]; parameters in closed
-          // form from the suffix norms ts_j = |d[j..n-1]|
-          float ss = wave_suffix_sum(dm * dm, lane);
-          if (wave == 0) ss += zhi;
-          const float ts = sqrtf(ss);
-          float cj = 1.f, sj = 0.f;
-          if (v > q && v < n) {
-            const float dprev = sh.vbuf[v - 1];
-            const float tp2 = fmaf(dprev, dprev, ss);  // ts_{v-1}^2
-            if (tp2 > 0.f) {
-              const float ri = rsqrtf(tp2);
-              cj = dprev * ri;
-              sj = ((v == n - 1) ? dv : ts) * ri;
-            }
-          }
-          *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(cj, sj);
-          // new column q of R: R[v][q] = d_v (v < q), R[q][q] = ts_q (d_q when q = n - 1)
-          {
-            const int offq = rcol(q);
-            if (v < q) sh.P[offq + v] = dv;
-            if (v == q) sh.P[offq + q] = (q == n - 1) ? dv : ts;
-          }
-          bar();
-          static_for<0, NV - 1>([&](auto IC) {
-            constexpr int j = NV - 1 - decltype(IC)::value;  // NV-1 .. 1
-            if ((j & 7) == 0) __builtin_amdgcn_sched_barrier(0);
-            if ((unsigned)(j - q - 1) < (unsigned)(n - q - 1)) {  // q < j < n
-              const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
-              const float a0 = slot[j - 1], b0 = slot[j];
-              slot[j - 1] = fmaf(cs2.x, a0, cs2.y * b0);
-              slot[j] = fmaf(-cs2.y, a0, cs2.x * b0);
-            }
-          });
-          pin(slot);
-          if (wave == 0) {
-            if (lane == q) { u_lo = up; a_lo = p; }
-            if (lane + 64 == q) { u_hi = up; a_hi = p; }
-          }
-          if (v == 0) sh.cflag[p] = 1;
-          q++;
-          break;
-        }
-        // ---- drop active constraint kk: shift positions kk+1..q-1 down, remove column kk of R
-        // and re-triangularise rows kk..q-1 with Givens rotations (wavefront 0, in place)
-        {
-          const int k = kk;
-          if (wave == 0) {
-            const int ak = (k < 64) ? rli(a_lo, k) : rli(a_hi, k - 64);
-            if (lane == 0) sh.cflag[ak] = 0;
-            const int alo_nx = lane_next_i(a_lo, a_lo);
-            const float ulo_nx = lane_next(u_lo, u_lo);
-            const int ahi_nx = lane_next_i(a_hi, a_hi);
-            const float uhi_nx = lane_next(u_hi, u_hi);
-            const int ahi0 = rli(a_hi, 0);
-            const float uhi0 = rl(u_hi, 0);
-            if (lane >= k && lane < q - 1) {
-              a_lo = (lane == 63) ? ahi0 : alo_nx;
-              u_lo = (lane == 63) ? uhi0 : ulo_nx;
-            }
-            if (lane + 64 >= k && lane + 64 < q - 1) { a_hi = ahi_nx; u_hi = uhi_nx; }
-            // new column c (k <= c <= q-2) = old column c+1. Lane l handles c = l and l + 64.
-            // Every read of an old entry precedes, in this wavefront's LDS order, the write that
-            // reuses its word (new column c overlays old column c).
-            const int clo = lane, chi = lane + 64;
-            const bool in_lo = clo >= k && clo <= q - 2;
-            const bool in_hi = chi >= k && chi <= q - 2;
-            float top_lo = in_lo ? sh.P[rcol(clo + 1) + k] : 0.f;
-            float top_hi = in_hi ? sh.P[rcol(chi + 1) + k] : 0.f;
-            lsync();
-            for (int r = 0; r < k; r++) {
-              const float xlo = in_lo ? sh.P[rcol(clo + 1) + r] : 0.f;
-              const float xhi = in_hi ? sh.P[rcol(chi + 1) + r] : 0.f;
-              lsync();
-              if (in_lo) sh.P[rcol(clo) + r] = xlo;
-              if (in_hi) sh.P[rcol(chi) + r] = xhi;
-              lsync();
-            }
-            for (int j = k; j <= q - 2; j++) {
-              const bool on_lo = in_lo && clo >= j, on_hi = in_hi && chi >= j;
-              const float bot_lo = on_lo ? sh.P[rcol(clo + 1) + j + 1] : 0.f;
-              const float bot_hi = on_hi ? sh.P[rcol(chi + 1) + j + 1] : 0.f;
-              lsync();
-              const float a0 = (j < 64) ? rl(top_lo, j) : rl(top_hi, j - 64);
-              const float b0 = (j < 64) ? rl(bot_lo, j) : rl(bot_hi, j - 64);
-              const float h = sqrtf(a0 * a0 + b0 * b0);
-              float cc = 1.f, sn = 0.f;
-              if (h > 0.f) { const float ih = fast_rcp(h); cc = a0 * ih; sn = b0 * ih; }
-              if (on_lo) {
-                sh.P[rcol(clo) + j] = fmaf(cc, top_lo, sn * bot_lo);
-                top_lo = fmaf(-sn, top_lo, cc * bot_lo);
-              }
-              if (on_hi) {
-                sh.P[rcol(chi) + j] = fmaf(cc, top_hi, sn * bot_hi);
-                top_hi = fmaf(-sn, top_hi, cc * bot_hi);
-              }
-              if (lane == 0) *reinterpret_cast<float2*>(&sh.cs[2 * j]) = make_float2(cc, sn);
-              lsync();
-            }
-          }
-          bar();
-          // the same rotations on J columns (j, j+1), j = k .. q-2
-          static_for<0, NV - 1>([&](auto JC) {
-            constexpr int j = decltype(JC)::value;  // 0 .. NV-2
-            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-            if ((unsigned)(j - k) < (unsigned)(q - 1 - k)) {  // k <= j < q-1
-              const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
-              const float x0 = slot[j], x1 = slot[j + 1];
-              slot[j] = fmaf(cs2.x, x0, cs2.y * x1);
-              slot[j + 1] = fmaf(-cs2.y, x0, cs2.x * x1);
-            }
-          });
-          pin(slot);
-          q--;
+        const float bt = -beta * tw;
+        // re-read w from LDS: without this point the compiler keeps all NV values of the first
+        // sweep's loads live for the second (a whole row of extra VGPRs)
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < NV; c += 4) {
+          const float4 w4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
+          slot[c + 0] = fmaf(bt, w4.x, slot[c + 0]);
+          slot[c + 1] = fmaf(bt, w4.y, slot[c + 1]);
+          slot[c + 2] = fmaf(bt, w4.z, slot[c + 2]);
+          slot[c + 3] = fmaf(bt, w4.w, slot[c + 3]);
+          CMPC_SWEEP_FENCE(c);
         }
       }
-      if (status != CMPC_OK) break;
+      // J columns (j, j+1) <- Givens chain j = 0 .. NV-2 (identity on an add)
+      static_for<0, NV - 1>([&](auto JC) {
+        constexpr int j = decltype(JC)::value;
+        const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+        const float x0 = slot[j], x1 = slot[j + 1];
+        slot[j] = fmaf(cs2.x, x0, cs2.y * x1);
+        slot[j + 1] = fmaf(-cs2.y, x0, cs2.x * x1);
+        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+      });
+      if (add) {
+        q++;
+        p = -1;
+      } else {
+        q--;
+      }
     }
   }
 

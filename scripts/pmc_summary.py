@@ -69,7 +69,8 @@ def main():
     dom = max(kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"]) if kernels else None
     summary = dict(tag=a.tag, horizon=a.horizon, batch=a.batch, kernels=kernels,
                    dominant=dom,
-                   hbm_bytes_per_launch=kernels.get("cmpc::cmpc_solve_reg_kernel<1>", {}).get(
+                   # the roofline's kernel: the 64-lane class (every instance with n <= 64)
+                   hbm_bytes_per_launch=kernels.get("cmpc::cmpc_solve_c1_kernel", {}).get(
                        "hbm_bytes_per_launch"),
                    note="FETCH_SIZE x2 (gfx950 half-count of wide reads) + WRITE_SIZE, KiB->B; "
                         "per launch, averaged over the profiled launches")
