@@ -1,6 +1,9 @@
-// cmpc_class2.hip — size class 2: fused condensation + friction-cone QP for instances with
-// 64 < n <= 128 reduced force variables (random contact tables at N = 10, trot at N = 11..21),
-// one 128-lane workgroup (two wavefronts) per instance, over class 1's overflow list.
+// cmpc_class2.hip — size classes 2a / 2b: fused condensation + friction-cone QP for instances
+// with 64 < n <= 96 (class 2a: random contact tables at N = 10, trot at N = 11..16) and
+// 96 < n <= 128 (class 2b: trot at N = 17..21) reduced force variables, one 128-lane workgroup
+// (two wavefronts) per instance, over the previous class's overflow list. The row width NV is a
+// template parameter: a 96-wide row fits the 256-VGPR budget of a 2-wave/SIMD kernel without
+// spilling, a 128-wide one does not, so most class-2 work at N = 10 runs in the narrow kernel.
 //
 // Same computation as cmpc_class1.hip — one call of the reference's solve_mpc()
 // (be2r_cmpc_unitree/src/controllers/convexMPC/SolverMPC.cpp:566-982) — with the same mapping:
@@ -24,40 +27,46 @@
 namespace cmpc {
 namespace {
 
-constexpr int NV = 128;
-constexpr int NG = NV / 4;
-constexpr int PSZ = 4 * NG * NV - 8 * NG * (NG - 1);  // packed rows r: columns [r & ~3, NV)
+constexpr int NT = 128;  // threads per workgroup: two wavefronts, lane v < NV owns row v
 constexpr int kNone = 0x7fffffff;
 
-__host__ __device__ constexpr int prow(int r) {
-  return 4 * (r >> 2) * NV - 8 * (r >> 2) * ((r >> 2) - 1) + (r & 3) * (NV - 4 * (r >> 2));
-}
-__host__ __device__ constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+// packed upper-row storage of an NV x NV matrix: row r holds columns [r & ~3, NV), 16-B aligned
+template <int NV>
+struct Geo {
+  static constexpr int NG = NV / 4;
+  static constexpr int PSZ = 4 * NG * NV - 8 * NG * (NG - 1);
+  __host__ __device__ static constexpr int prow(int r) {
+    return 4 * (r >> 2) * NV - 8 * (r >> 2) * ((r >> 2) - 1) + (r & 3) * (NV - 4 * (r >> 2));
+  }
+  __host__ __device__ static constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+  static_assert(NV % 4 == 0 && NV <= NT, "row width");
+  static_assert(NV * (NV + 1) / 2 <= PSZ, "R must fit in P");
+};
 // R (upper triangular, q x q) packed by columns: R[i][j] at rcol(j) + i, i <= j
 __device__ __forceinline__ int rcol(int j) { return (j * (j + 1)) >> 1; }
-static_assert(NV * (NV + 1) / 2 <= PSZ, "R must fit in P");
 
 constexpr int OFF_TRAJ = 0;
 constexpr int OFF_E = 12 * MAXN;
 constexpr int OFF_ZE = OFF_E + 16 * MAXN;
-static_assert(OFF_ZE + 16 * MAXN <= PSZ, "prep scratch must fit in P");
+static_assert(OFF_ZE + 16 * MAXN <= Geo<96>::PSZ, "prep scratch must fit in P");
 
-// 40.2 KB: four workgroups (eight wavefronts) per CU, matching the 256-VGPR budget
+// per-thread arrays are NT long (lanes v >= NV write them too); 25 KB (NV = 96) / 40 KB (128)
+template <int NV>
 struct SharedC2 {
-  float P[PSZ];
+  float P[Geo<NV>::PSZ];
   float BdtT[12][16];
-  float ibuf[NV];          // 1 / sqrt(d_k) of pivot k
-  float vbuf[NV];          // y, then the masked d (v >= q, v < n)
-  float dfull[NV];         // d = J' n+
-  float bufA[NV], bufB[NV];  // gradient border of pivot k (Cholesky); J rows ia, iz (QP)
-  float xs[NV];
-  float cs[2 * NV];        // Givens (c, s) per column pair
+  float ibuf[NT];          // 1 / sqrt(d_k) of pivot k
+  float vbuf[NT];          // y, then the masked d (v >= q, v < n)
+  float dfull[NT];         // d = J' n+
+  float bufA[NT], bufB[NT];  // gradient border of pivot k (Cholesky); J rows ia, iz (QP)
+  float xs[NT];
+  float cs[2 * NT];        // Givens (c, s) per column pair
   float redf[8];
   int redi[8];
   float sub[4 * MAXN];     // ub of each stance foot-step (gait * f_max)
   int sfs[4 * MAXN];       // stance foot-step ids, in order
   int blkbase[MAXN + 2];   // first reduced variable of each horizon step
-  unsigned char varblk[NV], varcol[NV];
+  unsigned char varblk[NT], varcol[NT];
   unsigned char stance[4 * MAXN];
   unsigned char cflag[2 * NV + 8];  // active flag per constraint id (6 per stance foot-step)
 };
@@ -82,11 +91,13 @@ __device__ __forceinline__ void pin(float (&x)[M]) {
     if (((c) & 15) == 12) __builtin_amdgcn_sched_barrier(0); \
   } while (0)
 
+template <int NV>
 __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KParams& P,
-                                         SharedC2& sh, float* __restrict__ fout,
+                                         SharedC2<NV>& sh, float* __restrict__ fout,
                                          uint8_t* __restrict__ st_out, int32_t* __restrict__ it_out,
                                          int* __restrict__ ovf_list, int* __restrict__ ovf_count,
                                          int inst) {
+  using G = Geo<NV>;
   const int v = threadIdx.x;
   const int lane = v & 63;
   const int wave = __builtin_amdgcn_readfirstlane(v >> 6);  // wave-uniform: scalar branches
@@ -113,7 +124,7 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
     nfs += __popcll(m);
   }
   const int n = 3 * nfs;
-  if (n > NV) {  // hand the instance to the general class
+  if (n > NV) {  // hand the instance to the next (wider) class
     if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
     return;
   }
@@ -132,12 +143,12 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
       for (int s = 0; s < nfs; s++) c += (sh.sfs[s] < 4 * v) ? 1 : 0;
       sh.blkbase[v] = 3 * c;
     }
-    for (int t = v; t < 6 * nfs; t += NV) sh.cflag[t] = 0;
-    for (int t = v; t < 12 * N; t += NV) sh.P[OFF_TRAJ + t] = rec[CMPC_REC_HDR + t];
+    for (int t = v; t < 6 * nfs; t += NT) sh.cflag[t] = 0;
+    for (int t = v; t < 12 * N; t += NT) sh.P[OFF_TRAJ + t] = rec[CMPC_REC_HDR + t];
   }
   Model md;
   make_model(rec, P.dt, md);
-  make_bdt<NV>(rec, md, v, sh.BdtT);
+  make_bdt<NT>(rec, md, v, sh.BdtT);
   bar();
   if (v < N) {
     float e[13];
@@ -186,7 +197,7 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
       gv = real ? 2.f * dot13(b, zk) : 0.f;  // qg = 2 B_qp' S (A_qp x0 + Q_qp f - X_d)
     }
     bar();  // every ZE read is done before P is overwritten
-    const int myrow = prow0(v);
+    const int myrow = G::prow0(v);
     float z[13];
 #pragma unroll
     for (int j = 0; j < 13; j++) z[j] = 0.f;
@@ -217,10 +228,10 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
   // ---- row v of H into registers (full symmetric; identity padding for v >= n) ----------
   float slot[NV + 1];
   {
-    const int myrow = prow0(v);
+    const int myrow = G::prow0(v);
     static_for<0, NV>([&](auto C) {
       constexpr int c = decltype(C)::value;
-      const int addr = (c >= v) ? myrow + c : prow0(c) + v;
+      const int addr = (c >= v) ? myrow + c : G::prow0(c) + v;
       const float x = sh.P[addr];
       slot[c] = (real && c < n) ? x : ((c == v) ? 1.f : 0.f);
       if ((c & 7) == 7) __builtin_amdgcn_sched_barrier(0);
@@ -235,9 +246,9 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int c0 = k & ~3;
-    constexpr int rk = prow(k);
+    constexpr int rk = G::prow(k);
     if (k < n) {
-      if (v >= c0) sh.P[rk + v - c0] = (v >= k) ? slot[k] : 0.f;
+      if (v >= c0 && v < NV) sh.P[rk + v - c0] = (v >= k) ? slot[k] : 0.f;
       if (v == k) sh.bufA[k] = slot[NV];
       bar();
       float d = sh.P[rk + k - c0];
@@ -269,7 +280,7 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int c0 = k & ~3;
-    constexpr int rk = prow(k);
+    constexpr int rk = G::prow(k);
     if (k < n) {
       lsync();
       const float inv = sh.ibuf[k];
@@ -562,11 +573,11 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
   // ---- scatter (q_soln layout 12 k + 3 leg + axis, swing -> 0) staged in LDS, coalesced out
   const bool ok = (status == CMPC_OK);
   bar();
-  for (int t = v; t < 12 * N; t += NV) sh.P[t] = 0.f;
+  for (int t = v; t < 12 * N; t += NT) sh.P[t] = 0.f;
   bar();
   if (ok && v < n) sh.P[12 * sh.varblk[v] + sh.varcol[v]] = xv;
   bar();
-  for (int t = 4 * v; t < 12 * N; t += 4 * NV)
+  for (int t = 4 * v; t < 12 * N; t += 4 * NT)
     *reinterpret_cast<float4*>(&fout[t]) = *reinterpret_cast<const float4*>(&sh.P[t]);
   if (v == 0) {
     st_out[0] = (uint8_t)status;
@@ -576,26 +587,34 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
 
 }  // namespace
 
-// One workgroup per entry of class 1's overflow list; the grid is sized for the worst case
-// (the list length is only known on the device) and surplus workgroups exit at once.
-__global__ __launch_bounds__(NV, CMPC_W2_WAVES_PER_EU) void cmpc_solve_c2_kernel(
+// One workgroup per entry of the previous class's overflow list; the grid is sized for the worst
+// case (the list length is only known on the device) and surplus workgroups exit at once.
+template <int NV>
+__global__ __launch_bounds__(NT, CMPC_W2_WAVES_PER_EU) void cmpc_solve_c2_kernel(
     const float* __restrict__ recs, KParams P, float* __restrict__ forces,
     uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
     const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
-  __shared__ SharedC2 sh;
+  __shared__ SharedC2<NV> sh;
   const int t = blockIdx.x;
   if (t >= *in_count) return;
   const int inst = in_list[t];
-  solve_c2(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
-           status + inst, iters ? iters + inst : nullptr, ovf_list, ovf_count, inst);
+  solve_c2<NV>(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
+               status + inst, iters ? iters + inst : nullptr, ovf_list, ovf_count, inst);
 }
 
-hipError_t launch_class2(const float* d_recs, int batch, const KParams& P, float* d_forces,
-                         uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
-                         int* ovf_list, int* ovf_count, int grid, hipStream_t stream) {
+hipError_t launch_class2(int width, const float* d_recs, int batch, const KParams& P,
+                         float* d_forces, uint8_t* d_status, int32_t* d_iters, const int* in_list,
+                         const int* in_count, int* ovf_list, int* ovf_count, int grid,
+                         hipStream_t stream) {
   (void)batch;
-  hipLaunchKernelGGL(cmpc_solve_c2_kernel, dim3(grid), dim3(NV), 0, stream, d_recs, P, d_forces,
-                     d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
+  if (width == 96)
+    hipLaunchKernelGGL(cmpc_solve_c2_kernel<96>, dim3(grid), dim3(NT), 0, stream, d_recs, P,
+                       d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
+  else if (width == 128)
+    hipLaunchKernelGGL(cmpc_solve_c2_kernel<128>, dim3(grid), dim3(NT), 0, stream, d_recs, P,
+                       d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -208,60 +208,63 @@ __device__ __forceinline__ void make_model(const float* __restrict__ rec, float 
     for (int j = 0; j < 3; j++) md.n1r[i * 3 + j] = dt * md.R[j * 3 + i];
 }
 
-// Bdt[s][c] for thread-strided entries t = s + 13 c (c = 3 leg + axis) -> BdtT[c][s]
-// (ct_ss_mats B_c rows 6..11: I_world^-1 [r]x, I/m; SolverMPC.cpp:267-276, m = 12 RobotState.h:26,
-// I_body = diag(.07, .26, .242) RobotState.h:25; I_world = R I_body R^T, SolverMPC.cpp:593)
+// Bdt[s][c] -> BdtT[c][s]: thread c < 12 (c = 3 leg + axis) builds column c, every row s
+// unrolled (constant indices only: a row-strided mapping turned the R lookups into a private
+// array on scratch). ct_ss_mats B_c rows 6..11: I_world^-1 [r]x, I/m; SolverMPC.cpp:267-276,
+// m = 12 RobotState.h:26, I_body = diag(.07, .26, .242) RobotState.h:25;
+// I_world = R I_body R^T, SolverMPC.cpp:593.
 template <int NT>
 __device__ __forceinline__ void make_bdt(const float* __restrict__ rec, const Model& md, int tid,
                                          float (*BdtT)[16]) {
-  const float Ib[3] = {.07f, 0.26f, 0.242f};
-  float Iw[9];
+  static_assert(NT >= 12, "one thread per force column");
+  if (tid < 12) {
+    const float Ib0 = .07f, Ib1 = 0.26f, Ib2 = 0.242f;
+    float Iw[9];
 #pragma unroll
-  for (int i = 0; i < 3; i++)
+    for (int i = 0; i < 3; i++)
 #pragma unroll
-    for (int j = 0; j < 3; j++)
-      Iw[i * 3 + j] = md.R[i * 3 + 0] * Ib[0] * md.R[j * 3 + 0] + md.R[i * 3 + 1] * Ib[1] * md.R[j * 3 + 1] +
-                      md.R[i * 3 + 2] * Ib[2] * md.R[j * 3 + 2];
-  const float c00 = Iw[4] * Iw[8] - Iw[5] * Iw[7];
-  const float c10 = Iw[5] * Iw[6] - Iw[3] * Iw[8];
-  const float c20 = Iw[3] * Iw[7] - Iw[4] * Iw[6];
-  const float idet = 1.f / (Iw[0] * c00 + Iw[1] * c10 + Iw[2] * c20);
-  float Ii[9];
-  Ii[0] = c00 * idet; Ii[1] = (Iw[2] * Iw[7] - Iw[1] * Iw[8]) * idet; Ii[2] = (Iw[1] * Iw[5] - Iw[2] * Iw[4]) * idet;
-  Ii[3] = c10 * idet; Ii[4] = (Iw[0] * Iw[8] - Iw[2] * Iw[6]) * idet; Ii[5] = (Iw[2] * Iw[3] - Iw[0] * Iw[5]) * idet;
-  Ii[6] = c20 * idet; Ii[7] = (Iw[1] * Iw[6] - Iw[0] * Iw[7]) * idet; Ii[8] = (Iw[0] * Iw[4] - Iw[1] * Iw[3]) * idet;
-  const float im = 1.f / 12.0f;
-  const float dt = md.dt, dt2 = md.dth, dt3 = md.dt * md.dt * md.dt / 6.f;
-  for (int t = tid; t < 13 * 12; t += NT) {
-    const int s = t % 13, c = t / 13;
-    const int b = c / 3, a = c % 3;
-    const float r0 = rec[CMPC_REC_R + 0 * 4 + b], r1 = rec[CMPC_REC_R + 1 * 4 + b], r2 = rec[CMPC_REC_R + 2 * 4 + b];
-    float cx[3];  // column a of [r]x
-    if (a == 0) { cx[0] = 0.f; cx[1] = r2; cx[2] = -r1; }
-    else if (a == 1) { cx[0] = -r2; cx[1] = 0.f; cx[2] = r0; }
-    else { cx[0] = r1; cx[1] = -r0; cx[2] = 0.f; }
+      for (int j = 0; j < 3; j++)
+        Iw[i * 3 + j] = md.R[i * 3 + 0] * Ib0 * md.R[j * 3 + 0] + md.R[i * 3 + 1] * Ib1 * md.R[j * 3 + 1] +
+                        md.R[i * 3 + 2] * Ib2 * md.R[j * 3 + 2];
+    const float c00 = Iw[4] * Iw[8] - Iw[5] * Iw[7];
+    const float c10 = Iw[5] * Iw[6] - Iw[3] * Iw[8];
+    const float c20 = Iw[3] * Iw[7] - Iw[4] * Iw[6];
+    const float idet = 1.f / (Iw[0] * c00 + Iw[1] * c10 + Iw[2] * c20);
+    float Ii[9];
+    Ii[0] = c00 * idet; Ii[1] = (Iw[2] * Iw[7] - Iw[1] * Iw[8]) * idet; Ii[2] = (Iw[1] * Iw[5] - Iw[2] * Iw[4]) * idet;
+    Ii[3] = c10 * idet; Ii[4] = (Iw[0] * Iw[8] - Iw[2] * Iw[6]) * idet; Ii[5] = (Iw[2] * Iw[3] - Iw[0] * Iw[5]) * idet;
+    Ii[6] = c20 * idet; Ii[7] = (Iw[1] * Iw[6] - Iw[0] * Iw[7]) * idet; Ii[8] = (Iw[0] * Iw[4] - Iw[1] * Iw[3]) * idet;
+    const float im = 1.f / 12.0f;
+    const float dt = md.dt, dt2 = md.dth, dt3 = md.dt * md.dt * md.dt / 6.f;
+    const int c = tid;
+    const int b = c / 3, a = c - 3 * (c / 3);
+    const float r0 = rec[CMPC_REC_R + 0 * 4 + b], r1 = rec[CMPC_REC_R + 1 * 4 + b],
+                r2 = rec[CMPC_REC_R + 2 * 4 + b];
+    // column a of [r]x
+    const float cx0 = (a == 0) ? 0.f : (a == 1) ? -r2 : r1;
+    const float cx1 = (a == 0) ? r2 : (a == 1) ? 0.f : -r0;
+    const float cx2 = (a == 0) ? -r1 : (a == 1) ? r0 : 0.f;
     float T[3];  // B_c[6+i][c] = (I_inv [r]x)[i][a]
 #pragma unroll
-    for (int i = 0; i < 3; i++) T[i] = Ii[i * 3 + 0] * cx[0] + Ii[i * 3 + 1] * cx[1] + Ii[i * 3 + 2] * cx[2];
-    const float b9 = (a == 0) ? im : 0.f;  // B_c[9][c]
-    float val = 0.f;
-    if (s < 3) {
-      const float c0 = (s == 0) ? md.R[0] : (s == 1) ? md.R[1] : md.R[2];
-      const float c1 = (s == 0) ? md.R[3] : (s == 1) ? md.R[4] : md.R[5];
-      const float c2 = (s == 0) ? md.R[6] : (s == 1) ? md.R[7] : md.R[8];
-      val = dt2 * (c0 * T[0] + c1 * T[1] + c2 * T[2]);
-    } else if (s < 6) {
-      val = dt2 * (((s - 3) == a) ? im : 0.f);
-      if (s == 5) val += dt3 * md.xdrag * b9;
-    } else if (s < 9) {
-      val = dt * ((s == 6) ? T[0] : (s == 7) ? T[1] : T[2]);
-    } else if (s < 12) {
-      val = dt * (((s - 9) == a) ? im : 0.f);
-      if (s == 11) val += dt2 * md.xdrag * b9;
-    }
-    BdtT[c][s] = val;
+    for (int i = 0; i < 3; i++) T[i] = Ii[i * 3 + 0] * cx0 + Ii[i * 3 + 1] * cx1 + Ii[i * 3 + 2] * cx2;
+    const float e0 = (a == 0) ? im : 0.f, e1 = (a == 1) ? im : 0.f, e2 = (a == 2) ? im : 0.f;
+    float* col = BdtT[c];
+#pragma unroll
+    for (int s = 0; s < 3; s++)  // dt^2/2 * N1-part: R^T (I_inv [r]x)
+      col[s] = dt2 * (md.R[0 * 3 + s] * T[0] + md.R[1 * 3 + s] * T[1] + md.R[2 * 3 + s] * T[2]);
+    col[3] = dt2 * e0;
+    col[4] = dt2 * e1;
+    col[5] = dt2 * e2 + dt3 * md.xdrag * e0;
+#pragma unroll
+    for (int s = 0; s < 3; s++) col[6 + s] = dt * T[s];
+    col[9] = dt * e0;
+    col[10] = dt * e1;
+    col[11] = dt * e2 + dt2 * md.xdrag * e0;
+    col[12] = 0.f;
+    col[13] = 0.f;
+    col[14] = 0.f;
+    col[15] = 0.f;
   }
-  for (int t = tid; t < 12 * 3; t += NT) BdtT[t / 3][13 + t % 3] = 0.f;
 }
 
 // e_i = Adt^{i+1} x0 + sum_{k<=i} Adt^k Qdt f - X_d,i for step i (SolverMPC.cpp:592, 633-642,

@@ -21,7 +21,7 @@ struct KParams {
 };
 
 // Scratch ints needed by launch_solve for max_batch instances.
-inline size_t work_ints(int max_batch) { return 4 + 2 * (size_t)max_batch; }
+inline size_t work_ints(int max_batch) { return 4 + 3 * (size_t)max_batch; }
 // Workgroups of the general class (persistent over its overflow list) and its global slabs.
 inline int classg_grid(int max_batch) { return max_batch < 512 ? max_batch : 512; }
 size_t classg_scratch_floats(int horizon, int grid);
@@ -35,9 +35,11 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
 hipError_t launch_class1(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
-hipError_t launch_class2(const float* d_recs, int batch, const KParams& P, float* d_forces,
-                         uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
-                         int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
+// width: row width of the 2-wavefront class, 96 (class 2a) or 128 (class 2b)
+hipError_t launch_class2(int width, const float* d_recs, int batch, const KParams& P,
+                         float* d_forces, uint8_t* d_status, int32_t* d_iters, const int* in_list,
+                         const int* in_count, int* ovf_list, int* ovf_count, int grid,
+                         hipStream_t stream);
 hipError_t launch_classg(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          float* scratch, int grid, hipStream_t stream);
