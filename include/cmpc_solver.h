@@ -80,6 +80,44 @@
 #define CMPC_EST_PARAMS   804 /* double[4]: est_stat, est_amp, est_freq, est_phase              */
 #define CMPC_EST_WORDS    816
 
+/* ------------------------------------------------------------------------------------------ */
+/* Batched input assembly: locomotion-controller state (fp32 words).  */
+/* The inputs and persistent state of ConvexMPCLocomotion::run's MPC side                     */
+/* (ConvexMPCLocomotion.cpp:100-123, 204-257, 334-339, 511-586, 612-633, 786-818).            */
+/* Words marked "state" are read and written back by cmpc_batch_assemble; int32 words are     */
+/* bit-cast into the fp32 array.                                                               */
+/* ------------------------------------------------------------------------------------------ */
+#define CMPC_LOCO_POS      0   /* seResult.position[3]                                         */
+#define CMPC_LOCO_ZGT      3   /* ground_truth_position[2]: p[2] of the solve (:628)           */
+#define CMPC_LOCO_Q        4   /* seResult.orientation (w,x,y,z)                               */
+#define CMPC_LOCO_RPY      8   /* seResult.rpy[3]                                              */
+#define CMPC_LOCO_VW       11  /* seResult.vWorld[3]                                           */
+#define CMPC_LOCO_WW       14  /* seResult.omegaWorld[3]                                       */
+#define CMPC_LOCO_PFOOT    17  /* pFoot[4][3], world frame, leg-major (:234)                   */
+#define CMPC_LOCO_CMD      29  /* x_vel_cmd, y_vel_cmd, _yaw_turn_rate (scaled sticks, :108-114)*/
+#define CMPC_LOCO_HEIGHT   32  /* _body_height                                                 */
+#define CMPC_LOCO_VDES     33  /* state: filtered _x_vel_des, _y_vel_des (:116-117)            */
+#define CMPC_LOCO_WPD      35  /* state: world_position_desired x, y (:239, :537-552)          */
+#define CMPC_LOCO_RPYINT   37  /* state: rpy_int[0], rpy_int[1] (:218-228)                     */
+#define CMPC_LOCO_XCI      39  /* state: x_comp_integral (:809-818)                            */
+#define CMPC_LOCO_COUNTER  40  /* state, int32: iterationCounter                               */
+#define CMPC_LOCO_GAIT     41  /* int32: OffsetDurationGait P, offsets[4], durations[4]        */
+#define CMPC_LOCO_FLAGS    50  /* state, uint32: CMPC_LOCO_OMNI | STANDING | PRONK | FIRST     */
+#define CMPC_LOCO_STAND    51  /* stand_traj x, y, yaw (:146-151; stand_traj[0], [1], [5])     */
+#define CMPC_LOCO_WORDS    56
+#define CMPC_LOCO_OMNI     1u  /* omniMode: v_des is already in the world frame (:211)         */
+#define CMPC_LOCO_STANDING 2u  /* current_gait == 4: stand trajectory (:527-533)               */
+#define CMPC_LOCO_PRONK    4u  /* gaitNumber == 8 (pacing): roll compensation off (:230)      */
+#define CMPC_LOCO_FIRST    8u  /* firstRun: world_position_desired = position (:249-256)       */
+
+/* Batch-shared controller constants. */
+typedef struct cmpc_loco_params {
+  float dt;               /* control tick (s); dtMPC = dt * iters_between_mpc                   */
+  int   iters_between_mpc;/* _iterationsBetweenMPC                                             */
+  float x_drag_gain;      /* _dyn_params->cmpc_x_drag                                          */
+  int   pad;
+} cmpc_loco_params;
+
 /* Per-instance status (batched API). The reference has no status: on qpOASES failure it prints
  * "failed to solve!" and leaves stale forces (SolverMPC.cpp:964-968). Documented deviation:
  * forces are zero when status != CMPC_OK. */
@@ -169,6 +207,16 @@ CMPC_EXTERNC int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int 
 CMPC_EXTERNC int cmpc_batch_estimate(cmpc_batch* h, float* d_est, const float* d_logs,
                                      const float* d_fext3, const float* d_time, float sim_time,
                                      float* d_records, float* d_fext6, int batch);
+/* One control tick of every instance's locomotion controller (batched
+ * ConvexMPCLocomotion::run MPC side): updates the state words of d_loco [batch *
+ * CMPC_LOCO_WORDS]; where an MPC step is due (iterationCounter % iters_between_mpc == 0 after
+ * the increment) writes the instance's solve record d_records[i] (the arguments the reference
+ * passes to update_problem_data_floats: p, v, q, w, r, rpy, trajAll, gait table, x_drag) and
+ * d_due[i] = 1, else leaves the record and sets d_due[i] = 0. Gait rows i < N use
+ * (i + _iteration + 1) mod P, i.e. the table repeats for N > P where the reference would read
+ * past its P-row table. Asynchronous on the handle's stream. */
+CMPC_EXTERNC int cmpc_batch_assemble(cmpc_batch* h, float* d_loco, const cmpc_loco_params* lp,
+                                     float* d_records, uint8_t* d_due, int batch);
 /* Measurement hooks: record HIP events around each size-class launch of the next `steps`
  * solves; read back per-launch ms pairs [class1, class2] and class 1's overflow count (the
  * number of instances handed to the 2-wave class in the last solve). Synchronises. */

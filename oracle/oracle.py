@@ -191,3 +191,134 @@ def est_step(state: np.ndarray, f3: float, t: float):
     use = ctypes.c_int()
     f = lib().oracle_est_step(_fp(state), float(f3), float(t), ctypes.byref(use))
     return f, bool(use.value)
+
+
+# ---------------------------------------------------------------------------------------------
+# Batched input assembly (cmpc_batch_assemble): one control tick of ConvexMPCLocomotion::run's
+# MPC side per instance, restated in scalar fp32 (numpy float32: every operation rounds to fp32
+# in the reference's evaluation order; the kernel compiles with fp contraction off, so the two
+# agree bit for bit). Parity: anchored on the reference's own code only (no reference test
+# covers the controller), i.e. the citations below.
+# ---------------------------------------------------------------------------------------------
+def assemble_tick(loco: np.ndarray, horizon: int, dt: float, iters: int, x_drag_gain: float,
+                  rec_words: int):
+    """-> (new loco row, record row or None). ``loco`` is one CMPC_LOCO_WORDS float32 row."""
+    import importlib
+    R_ = importlib.import_module("quad-periodic-mpc_amd.records")
+    f32 = np.float32
+    s = loco.astype(np.float32).copy()
+    ints = s.view(np.int32)
+    flags = int(s.view(np.uint32)[R_.LOCO_FLAGS])
+    omni, standing, pronk = bool(flags & 1), bool(flags & 2), bool(flags & 4)
+    dt = f32(dt)
+    pos = [s[R_.LOCO_POS + k] for k in range(3)]
+    vw0, vw1 = s[R_.LOCO_VW], s[R_.LOCO_VW + 1]
+    rpy = [s[R_.LOCO_RPY + k] for k in range(3)]
+    # _SetupCommand, ConvexMPCLocomotion.cpp:100-123
+    filt = f32(0.1)
+    vdx = s[R_.LOCO_VDES] * (f32(1) - filt) + s[R_.LOCO_CMD] * filt
+    vdy = s[R_.LOCO_VDES + 1] * (f32(1) - filt) + s[R_.LOCO_CMD + 1] * filt
+    yaw_rate = s[R_.LOCO_CMD + 2]
+    roll_des = pitch_des = yaw_des = f32(0)
+    s[R_.LOCO_VDES], s[R_.LOCO_VDES + 1] = vdx, vdy
+    # setIterations, Gait.cpp:218-226
+    counter = int(ints[R_.LOCO_COUNTER])
+    P = int(ints[R_.LOCO_GAIT])
+    iteration = (counter // iters) % P
+    # v_des_world = rBody^T v_des_robot (:210-211; orientation_tools.h:195-211)
+    e0, e1, e2, e3 = (s[R_.LOCO_Q + k] for k in range(4))
+    two, one = f32(2), f32(1)
+    if omni:
+        vdw0, vdw1 = vdx, vdy
+    else:
+        R00 = one - two * (e2 * e2 + e3 * e3)
+        R01 = two * (e1 * e2 - e0 * e3)
+        R02 = two * (e1 * e3 + e0 * e2)
+        R10 = two * (e1 * e2 + e0 * e3)
+        R11 = one - two * (e1 * e1 + e3 * e3)
+        R12 = two * (e2 * e3 - e0 * e1)
+        vdw0 = R00 * vdx + R01 * vdy + R02 * f32(0)
+        vdw1 = R10 * vdx + R11 * vdy + R12 * f32(0)
+    # rpy_int / rpy_comp (:218-230)
+    ri0, ri1 = s[R_.LOCO_RPYINT], s[R_.LOCO_RPYINT + 1]
+    if abs(vw0) > f32(0.2):
+        ri1 = ri1 + dt * (pitch_des - rpy[1]) / vw0
+    if abs(vw1) > f32(0.1):
+        ri0 = ri0 + dt * (roll_des - rpy[0]) / vw1
+    ri0 = min(max(ri0, f32(-0.25)), f32(0.25))
+    ri1 = min(max(ri1, f32(-0.25)), f32(0.25))
+    comp1 = vw0 * ri1
+    comp0 = vw1 * ri0 * (f32(0) if pronk else f32(1))
+    s[R_.LOCO_RPYINT], s[R_.LOCO_RPYINT + 1] = ri0, ri1
+    # world_position_desired (:237-257)
+    wx, wy = s[R_.LOCO_WPD], s[R_.LOCO_WPD + 1]
+    if not standing:
+        wx = wx + dt * vdw0
+        wy = wy + dt * vdw1
+    if flags & 8:
+        wx, wy = pos[0], pos[1]
+        flags &= ~8
+    # iterationCounter++ (:334); updateMPCIfNeeded (:514)
+    nc = counter + 1
+    ints[R_.LOCO_COUNTER] = nc
+    rec = None
+    if nc % iters == 0:
+        dtm = dt * f32(iters)
+        N = horizon
+        rec = np.zeros(rec_words, np.float32)
+        if standing:  # :529-533
+            t0 = [roll_des, pitch_des, s[R_.LOCO_STAND + 2], s[R_.LOCO_STAND], s[R_.LOCO_STAND + 1]]
+        else:         # :537-566
+            mpe = f32(0.1)
+            xs, ys = wx, wy
+            if xs - pos[0] > mpe:
+                xs = pos[0] + mpe
+            if pos[0] - xs > mpe:
+                xs = pos[0] - mpe
+            if ys - pos[1] > mpe:
+                ys = pos[1] + mpe
+            if pos[1] - ys > mpe:
+                ys = pos[1] - mpe
+            wx, wy = xs, ys
+            t0 = [comp0, comp1, yaw_des, xs, ys]
+        z = f32(0)
+        t0 += [s[R_.LOCO_HEIGHT], z, z, z if standing else yaw_rate, z if standing else vdw0,
+               z if standing else vdw1, z]
+        traj = np.tile(np.array(t0, np.float32), N).reshape(N, 12)
+        if not standing:  # :568-585
+            traj[0, 2] = rpy[2]
+            for i in range(1, N):
+                traj[i, 3] = traj[i - 1, 3] + dtm * vdw0
+                traj[i, 4] = traj[i - 1, 4] + dtm * vdw1
+                traj[i, 2] = traj[i - 1, 2] + dtm * yaw_rate
+        rec[R_.REC_HDR:R_.REC_HDR + 12 * N] = traj.reshape(-1)
+        # getMpcTable (Gait.cpp:159-188), rows periodic in P
+        offs = ints[R_.LOCO_GAIT + 1:R_.LOCO_GAIT + 5]
+        durs = ints[R_.LOCO_GAIT + 5:R_.LOCO_GAIT + 9]
+        gait = np.zeros(4 * N, np.uint8)
+        for i in range(N):
+            it = (i + iteration + 1) % P
+            for j in range(4):
+                prog = it - int(offs[j])
+                if prog < 0:
+                    prog += P
+                gait[4 * i + j] = 1 if prog < int(durs[j]) else 0
+        rec[R_.REC_HDR + 12 * N:R_.REC_HDR + 13 * N] = gait.view(np.float32)
+        # solveDenseMPC inputs (:619-633, :786-790)
+        zgt = s[R_.LOCO_ZGT]
+        rec[R_.REC_P:R_.REC_P + 3] = [pos[0], pos[1], zgt]
+        rec[R_.REC_V:R_.REC_V + 3] = s[R_.LOCO_VW:R_.LOCO_VW + 3]
+        rec[R_.REC_W:R_.REC_W + 3] = s[R_.LOCO_WW:R_.LOCO_WW + 3]
+        rec[R_.REC_RPY:R_.REC_RPY + 3] = s[R_.LOCO_RPY:R_.LOCO_RPY + 3]
+        rec[R_.REC_Q:R_.REC_Q + 4] = s[R_.LOCO_Q:R_.LOCO_Q + 4]
+        for t in range(12):
+            rec[R_.REC_R + t] = s[R_.LOCO_PFOOT + 3 * (t % 4) + t // 4] - pos[t // 4]
+        xci = s[R_.LOCO_XCI]
+        rec[R_.REC_XDRAG] = xci
+        pz_err = zgt - s[R_.LOCO_HEIGHT]
+        if vw0 > f32(0.3) or vw0 < f32(-0.3):
+            xci = xci + f32(x_drag_gain) * pz_err * dtm / vw0
+        s[R_.LOCO_XCI] = xci
+    s[R_.LOCO_WPD], s[R_.LOCO_WPD + 1] = wx, wy
+    s.view(np.uint32)[R_.LOCO_FLAGS] = flags
+    return s, rec

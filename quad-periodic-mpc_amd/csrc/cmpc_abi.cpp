@@ -10,6 +10,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -42,6 +43,8 @@ struct cmpc_batch {
   float* d_forces = nullptr;
   uint8_t* d_status = nullptr;
   int32_t* d_iters = nullptr;
+  // side streams + fork/join events for the wider size classes (cmpc_launch.hip)
+  cmpc::LaunchCtx ctx;
   // optional per-launch timing (cmpc_batch_enable_timing)
   std::vector<hipEvent_t> ev;
   int ev_steps = 0, ev_next = 0;
@@ -118,6 +121,18 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
     if (e != hipSuccess) { delete h; return fail("hipStreamCreate", e); }
     h->own_stream = true;
   }
+  // side streams at the highest priority: their few, long class-2 solves are dispatched ahead
+  // of class 1's queue, so they finish inside class 1's run instead of forming a tail
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (const char* pe = getenv("CMPC_SIDE_PRIORITY"); pe && atoi(pe) == 0) prio_hi = prio_lo;
+  for (int j = 0; j < cmpc::kSideStreams; j++) {
+    e = hipStreamCreateWithPriority(&h->ctx.side[j], hipStreamNonBlocking, prio_hi);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.join[j], hipEventDisableTiming);
+    if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("side streams", e); }
+  }
+  e = hipEventCreateWithFlags(&h->ctx.fork, hipEventDisableTiming);
+  if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("fork event", e); }
   e = hipMalloc(&h->d_work, sizeof(int) * cmpc::work_ints(max_batch));
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("hipMalloc(work)", e); }
   {
@@ -143,6 +158,11 @@ extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (h->d_status) (void)hipFree(h->d_status);
   if (h->d_iters) (void)hipFree(h->d_iters);
   for (auto e : h->ev) (void)hipEventDestroy(e);
+  for (int j = 0; j < cmpc::kSideStreams; j++) {
+    if (h->ctx.side[j]) (void)hipStreamDestroy(h->ctx.side[j]);
+    if (h->ctx.join[j]) (void)hipEventDestroy(h->ctx.join[j]);
+  }
+  if (h->ctx.fork) (void)hipEventDestroy(h->ctx.fork);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -159,7 +179,7 @@ extern "C" int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int batch
   hipEvent_t* ev = nullptr;
   if (h->ev_steps > 0 && h->ev_next < h->ev_steps) ev = &h->ev[3 * h->ev_next++];
   hipError_t e = cmpc::launch_solve(d_records, batch, h->kp, d_forces, d_status, d_iters, h->d_work,
-                                    h->max_batch, h->d_gscratch, h->stream, ev);
+                                    h->max_batch, h->d_gscratch, h->stream, h->ctx, ev);
   if (e != hipSuccess) return fail("launch_solve", e);
   return 0;
 }
@@ -175,6 +195,20 @@ extern "C" int cmpc_batch_estimate(cmpc_batch* h, float* d_est, const float* d_l
   hipError_t e = cmpc::launch_estimate(d_est, d_logs, d_fext3, d_time, sim_time, d_records,
                                        h->kp.rec_words, d_fext6, h->d_gauss, batch, h->stream);
   if (e != hipSuccess) return fail("launch_estimate", e);
+  return 0;
+}
+
+extern "C" int cmpc_batch_assemble(cmpc_batch* h, float* d_loco, const cmpc_loco_params* lp,
+                                   float* d_records, uint8_t* d_due, int batch) {
+  if (!h || !lp || batch < 0 || batch > h->max_batch ||
+      (batch && (!d_loco || !d_records || !d_due)) || !(lp->dt > 0.f) ||
+      lp->iters_between_mpc < 1) {
+    g_last_error = "cmpc_batch_assemble: bad arguments";
+    return -1;
+  }
+  cmpc::LocoParams kp{lp->dt, lp->iters_between_mpc, lp->x_drag_gain, h->kp.N, h->kp.rec_words};
+  hipError_t e = cmpc::launch_assemble(d_loco, kp, d_records, d_due, batch, h->stream);
+  if (e != hipSuccess) return fail("launch_assemble", e);
   return 0;
 }
 

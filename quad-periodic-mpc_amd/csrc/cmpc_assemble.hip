@@ -1,0 +1,199 @@
+// cmpc_assemble.hip — batched on-device MPC input assembly.
+//
+// One thread advances one instance's locomotion controller by one control tick, doing exactly
+// the MPC-input side of ConvexMPCLocomotion::run (be2r_cmpc_unitree/src/controllers/convexMPC/
+// ConvexMPCLocomotion.cpp):
+//   _SetupCommand           :100-123  first-order command filter (filter 0.1), yaw/roll/pitch_des 0
+//   setIterations           Gait.cpp:218-226  _iteration = (counter / iters) % P
+//   v_des_world             :210-211  rBody^T v_des_robot (omniMode: v_des_robot)
+//   rpy_int / rpy_comp      :218-230  integral pitch / roll compensation, clamped to +-0.25
+//   world_position_desired  :237-257  += dt v_des_world (not standing); first run: = position
+//   iterationCounter++      :334
+//   getMpcTable             Gait.cpp:159-188 (rows i < N; periodic for N > P)
+//   updateMPCIfNeeded       :511-586  every `iters` ticks: the trajAll reference
+//   solveDenseMPC inputs    :619-633, :786-790, :806-818  p = (x, y, z_groundtruth), r = pFoot - p,
+//                           x_drag = x_comp_integral, then the x_comp_integral update
+// and, when an MPC step is due, writes the instance's solve record (include/cmpc_solver.h) for
+// cmpc_batch_solve: the record the reference would hand to update_problem_data_floats.
+//
+// The work is a few hundred scalar flops per instance: the kernel is HBM-bound (224 B of state
+// read + written, one 16-B-aligned record written per due instance). Floating-point
+// contraction is off so results are bit-identical to the fp32 restatement in oracle/oracle.py.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cmpc_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace cmpc {
+namespace {
+
+__global__ __launch_bounds__(256) void cmpc_assemble_kernel(float* __restrict__ loco, LocoParams lp,
+                                                            float* __restrict__ recs,
+                                                            uint8_t* __restrict__ due, int batch) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch) return;
+  float* s = loco + (size_t)i * CMPC_LOCO_WORDS;
+  const float dt = lp.dt;
+  const int iters = lp.iters_between_mpc;
+  const int N = lp.horizon;
+  const uint32_t flags = __float_as_uint(s[CMPC_LOCO_FLAGS]);
+  const bool omni = flags & CMPC_LOCO_OMNI, standing = flags & CMPC_LOCO_STANDING,
+             pronk = flags & CMPC_LOCO_PRONK;
+  const float pos0 = s[CMPC_LOCO_POS + 0], pos1 = s[CMPC_LOCO_POS + 1], pos2 = s[CMPC_LOCO_POS + 2];
+  const float vw0 = s[CMPC_LOCO_VW + 0], vw1 = s[CMPC_LOCO_VW + 1];
+  const float rpy0 = s[CMPC_LOCO_RPY + 0], rpy1 = s[CMPC_LOCO_RPY + 1], rpy2 = s[CMPC_LOCO_RPY + 2];
+
+  // _SetupCommand (:114-122): _x_vel_des = _x_vel_des (1 - filter) + x_vel_cmd filter
+  const float filter = 0.1f;
+  const float vdx = s[CMPC_LOCO_VDES + 0] * (1.f - filter) + s[CMPC_LOCO_CMD + 0] * filter;
+  const float vdy = s[CMPC_LOCO_VDES + 1] * (1.f - filter) + s[CMPC_LOCO_CMD + 1] * filter;
+  const float yaw_rate = s[CMPC_LOCO_CMD + 2];
+  const float roll_des = 0.f, pitch_des = 0.f, yaw_des = 0.f;
+  s[CMPC_LOCO_VDES + 0] = vdx;
+  s[CMPC_LOCO_VDES + 1] = vdy;
+
+  // setIterations (Gait.cpp:218-226)
+  const int counter = __float_as_int(s[CMPC_LOCO_COUNTER]);
+  const int P = __float_as_int(s[CMPC_LOCO_GAIT + 0]);
+  const int iteration = (counter / iters) % P;
+
+  // v_des_world = rBody^T v_des_robot; rBody^T is quaternionToRotationMatrix before its
+  // transposeInPlace (common/Math/orientation_tools.h:195-211)
+  const float e0 = s[CMPC_LOCO_Q + 0], e1 = s[CMPC_LOCO_Q + 1], e2 = s[CMPC_LOCO_Q + 2],
+              e3 = s[CMPC_LOCO_Q + 3];
+  float vdw0 = vdx, vdw1 = vdy;
+  if (!omni) {
+    const float R00 = 1.f - 2.f * (e2 * e2 + e3 * e3), R01 = 2.f * (e1 * e2 - e0 * e3),
+                R02 = 2.f * (e1 * e3 + e0 * e2);
+    const float R10 = 2.f * (e1 * e2 + e0 * e3), R11 = 1.f - 2.f * (e1 * e1 + e3 * e3),
+                R12 = 2.f * (e2 * e3 - e0 * e1);
+    vdw0 = R00 * vdx + R01 * vdy + R02 * 0.f;
+    vdw1 = R10 * vdx + R11 * vdy + R12 * 0.f;
+  }
+
+  // rpy_int / rpy_comp (:218-230)
+  float ri0 = s[CMPC_LOCO_RPYINT + 0], ri1 = s[CMPC_LOCO_RPYINT + 1];
+  if (fabsf(vw0) > .2f) ri1 += dt * (pitch_des - rpy1) / vw0;
+  if (fabsf(vw1) > 0.1f) ri0 += dt * (roll_des - rpy0) / vw1;
+  ri0 = fminf(fmaxf(ri0, -.25f), .25f);
+  ri1 = fminf(fmaxf(ri1, -.25f), .25f);
+  const float comp1 = vw0 * ri1;
+  const float comp0 = vw1 * ri0 * (pronk ? 0.f : 1.f);
+  s[CMPC_LOCO_RPYINT + 0] = ri0;
+  s[CMPC_LOCO_RPYINT + 1] = ri1;
+
+  // world_position_desired (:237-257)
+  float wx = s[CMPC_LOCO_WPD + 0], wy = s[CMPC_LOCO_WPD + 1];
+  if (!standing) {
+    wx += dt * vdw0;
+    wy += dt * vdw1;
+  }
+  uint32_t nflags = flags;
+  if (flags & CMPC_LOCO_FIRST) {
+    wx = pos0;
+    wy = pos1;
+    nflags &= ~(uint32_t)CMPC_LOCO_FIRST;
+  }
+
+  // iterationCounter++ (:334); updateMPCIfNeeded (:514) tests the incremented counter
+  const int nc = counter + 1;
+  s[CMPC_LOCO_COUNTER] = __int_as_float(nc);
+  const bool mpc = (nc % iters) == 0;
+  const float dtMPC = dt * (float)iters;
+  float xci = s[CMPC_LOCO_XCI];
+  if (mpc) {
+    float* rec = recs + (size_t)i * lp.rec_words;
+    float traj0[12];
+    if (standing) {  // :529-533
+      traj0[0] = roll_des; traj0[1] = pitch_des; traj0[2] = s[CMPC_LOCO_STAND + 2];
+      traj0[3] = s[CMPC_LOCO_STAND + 0]; traj0[4] = s[CMPC_LOCO_STAND + 1];
+    } else {  // :537-566, desired xy kept within 0.1 of the measured position
+      const float max_pos_error = .1f;
+      float xs = wx, ys = wy;
+      if (xs - pos0 > max_pos_error) xs = pos0 + max_pos_error;
+      if (pos0 - xs > max_pos_error) xs = pos0 - max_pos_error;
+      if (ys - pos1 > max_pos_error) ys = pos1 + max_pos_error;
+      if (pos1 - ys > max_pos_error) ys = pos1 - max_pos_error;
+      wx = xs;
+      wy = ys;
+      traj0[0] = comp0; traj0[1] = comp1; traj0[2] = yaw_des; traj0[3] = xs; traj0[4] = ys;
+    }
+    traj0[5] = s[CMPC_LOCO_HEIGHT];
+    traj0[6] = 0.f; traj0[7] = 0.f;
+    traj0[8] = standing ? 0.f : yaw_rate;
+    traj0[9] = standing ? 0.f : vdw0;
+    traj0[10] = standing ? 0.f : vdw1;
+    traj0[11] = 0.f;
+    float* traj = rec + CMPC_REC_TRAJ(N);
+    float px = traj0[3], py = traj0[4], pyaw = rpy2;
+    for (int k = 0; k < N; k++) {  // :568-585
+#pragma unroll
+      for (int j = 0; j < 12; j++) traj[12 * k + j] = traj0[j];
+      if (!standing) {
+        if (k > 0) {
+          px = px + dtMPC * vdw0;
+          py = py + dtMPC * vdw1;
+          pyaw = pyaw + dtMPC * yaw_rate;
+        }
+        traj[12 * k + 2] = pyaw;
+        traj[12 * k + 3] = px;
+        traj[12 * k + 4] = py;
+      }
+    }
+    // getMpcTable (Gait.cpp:159-188) with the _iteration of this tick
+    uint32_t* gw = reinterpret_cast<uint32_t*>(rec + CMPC_REC_GAIT(N));
+    for (int k = 0; k < N; k++) {
+      const int it = (k + iteration + 1) % P;
+      uint32_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        int prog = it - __float_as_int(s[CMPC_LOCO_GAIT + 1 + j]);
+        if (prog < 0) prog += P;
+        if (prog < __float_as_int(s[CMPC_LOCO_GAIT + 5 + j])) word |= 1u << (8 * j);
+      }
+      gw[k] = word;
+    }
+    // solveDenseMPC inputs (:619-633, :786-790)
+    const float zgt = s[CMPC_LOCO_ZGT];
+    rec[CMPC_REC_P + 0] = pos0;
+    rec[CMPC_REC_P + 1] = pos1;
+    rec[CMPC_REC_P + 2] = zgt;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      rec[CMPC_REC_V + k] = s[CMPC_LOCO_VW + k];
+      rec[CMPC_REC_W + k] = s[CMPC_LOCO_WW + k];
+      rec[CMPC_REC_RPY + k] = s[CMPC_LOCO_RPY + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) rec[CMPC_REC_Q + k] = s[CMPC_LOCO_Q + k];
+    const float pp[3] = {pos0, pos1, pos2};
+#pragma unroll
+    for (int t = 0; t < 12; t++) rec[CMPC_REC_R + t] = s[CMPC_LOCO_PFOOT + 3 * (t % 4) + t / 4] - pp[t / 4];
+    rec[CMPC_REC_XDRAG] = xci;  // update_x_drag(x_comp_integral) precedes the update (:809)
+    rec[CMPC_REC_FEST3] = 0.f;
+    rec[CMPC_REC_FLAGS] = 0.f;
+    rec[31] = 0.f;
+    // x_comp_integral (:802, :813-818): pz_err uses p[2] = z_groundtruth
+    const float pz_err = zgt - s[CMPC_LOCO_HEIGHT];
+    if (vw0 > 0.3f || vw0 < -0.3f) xci += lp.x_drag_gain * pz_err * dtMPC / vw0;
+    s[CMPC_LOCO_XCI] = xci;
+  }
+  s[CMPC_LOCO_WPD + 0] = wx;
+  s[CMPC_LOCO_WPD + 1] = wy;
+  s[CMPC_LOCO_FLAGS] = __uint_as_float(nflags);
+  due[i] = mpc ? 1 : 0;
+}
+
+}  // namespace
+
+hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, uint8_t* d_due,
+                           int batch, hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cmpc_assemble_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_loco,
+                     lp, d_recs, d_due, batch);
+  return hipGetLastError();
+}
+
+}  // namespace cmpc

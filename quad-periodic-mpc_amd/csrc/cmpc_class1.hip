@@ -28,6 +28,22 @@
 #define CMPC_W1_WAVES_PER_EU 2
 #endif
 
+// Phase profiler (diagnostic builds only, -DCMPC_PHASE_PROF): lane 0 of every solved instance
+// adds the s_memtime cycles spent in each stage to g_c1_phase (scripts/phase_prof.py).
+#ifdef CMPC_PHASE_PROF
+__device__ unsigned long long g_c1_phase[8];
+#define C1_MARK(i)                              \
+  do {                                          \
+    const unsigned long long _n = clock64();    \
+    ph[i] += _n - t_last;                       \
+    t_last = _n;                                \
+  } while (0)
+#else
+#define C1_MARK(i) \
+  do {             \
+  } while (0)
+#endif
+
 namespace cmpc {
 namespace {
 
@@ -46,10 +62,10 @@ __device__ __forceinline__ int rcol(int j) { return (j * (j + 1)) >> 1; }
 static_assert(NV * (NV + 1) / 2 <= PSZ, "R must fit in P");
 
 // prep scratch inside P (P is not yet holding H while these are live)
-constexpr int OFF_TRAJ = 0;
-constexpr int OFF_E = 12 * MAXN;
+constexpr int OFF_E = 0;
 constexpr int OFF_ZE = OFF_E + 16 * MAXN;
-static_assert(OFF_ZE + 16 * MAXN <= PSZ, "prep scratch must fit in P");
+constexpr int OFF_REC = OFF_ZE + 16 * MAXN;  // LDS copy of the instance record (16-B aligned)
+static_assert(OFF_REC + CMPC_REC_WORDS(MAXN) <= PSZ, "prep scratch must fit in P");
 
 struct SharedC1 {
   float P[PSZ];
@@ -101,9 +117,23 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
                                          int inst) {
   const int v = threadIdx.x;
   const int N = P.N;
+#ifdef CMPC_PHASE_PROF
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_last = clock64();
+#endif
+  // ---- stage the record in LDS: one 16-B load per lane, so the whole prep waits on a single
+  // HBM round trip (record words are a multiple of 4, records 16-B aligned)
+  {
+    const float4* src = reinterpret_cast<const float4*>(rec);
+    float4* dst = reinterpret_cast<float4*>(&sh.P[OFF_REC]);
+    for (int t = v; t < (P.rec_words >> 2); t += 64) dst[t] = src[t];
+  }
+  lsync();
+  const float* srec = &sh.P[OFF_REC];
   // ---- stance table + elimination: eliminated iff |gait * f_max| < 0.01 (SolverMPC.cpp:869-894)
-  const unsigned char* gait = reinterpret_cast<const unsigned char*>(rec + CMPC_REC_HDR + 12 * N);
+  const unsigned char* gait = reinterpret_cast<const unsigned char*>(srec + CMPC_REC_HDR + 12 * N);
   int nfs = 0;
+  unsigned long long msk0 = 0ull, msk1 = 0ull;  // stance ballots of foot-steps 0..63, 64..127
   for (int c0 = 0; c0 < 4 * N; c0 += 64) {
     const int t = c0 + v;
     float ub = 0.f;
@@ -114,6 +144,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       sh.stance[t] = f ? 1 : 0;
     }
     const unsigned long long m = __ballot(f);
+    if (c0 == 0) msk0 = m; else msk1 = m;
     const int pre = __popcll(m & ((1ull << v) - 1ull));
     if (f) {
       sh.sfs[nfs + pre] = t;
@@ -123,7 +154,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   }
   const int n = 3 * nfs;
   if (n > NV) {  // hand the instance to the next size class
-    if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
+    if (v == 0 && ovf_list) ovf_list[atomicAdd(ovf_count, 1)] = inst;
     return;
   }
   lsync();
@@ -136,21 +167,21 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     }
     sh.varblk[v] = (unsigned char)kb;
     sh.varcol[v] = (unsigned char)kc;
-    if (v <= N) {
-      int c = 0;
-      for (int s = 0; s < nfs; s++) c += (sh.sfs[s] < 4 * v) ? 1 : 0;
-      sh.blkbase[v] = 3 * c;
+    if (v <= N) {  // stance foot-steps before step v: popcounts of the ballots
+      const int b0 = 4 * v, b1 = 4 * v - 64;
+      const unsigned long long lo = (b0 >= 64) ? msk0 : (msk0 & ((1ull << b0) - 1ull));
+      const unsigned long long hi = (b1 <= 0) ? 0ull : (msk1 & ((1ull << b1) - 1ull));
+      sh.blkbase[v] = 3 * (__popcll(lo) + __popcll(hi));
     }
     for (int t = v; t < 6 * nfs; t += 64) sh.cflag[t] = 0;
-    for (int t = v; t < 12 * N; t += 64) sh.P[OFF_TRAJ + t] = rec[CMPC_REC_HDR + t];
   }
   Model md;
-  make_model(rec, P.dt, md);
-  make_bdt<64>(rec, md, v, sh.BdtT);
+  make_model(srec, P.dt, md);
+  make_bdt<64>(srec, md, v, sh.BdtT);
   lsync();
   if (v < N) {
     float e[13];
-    state_error(rec, md, v, &sh.P[OFF_TRAJ + 12 * v], e);
+    state_error(srec, md, v, srec + CMPC_REC_HDR + 12 * v, e);
 #pragma unroll
     for (int j = 0; j < 13; j++) sh.P[OFF_E + 16 * v + j] = e[j];
   }
@@ -177,6 +208,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     }
   }
   lsync();
+  C1_MARK(0);
 
   // ---- condensation: lane v builds H[v][w] for w >= v into packed P, and its gradient g_v
   const bool real = v < n;
@@ -223,6 +255,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     }
   }
   lsync();
+  C1_MARK(1);
 
   // ---- row v of H into registers (full symmetric; identity padding for v >= n) ----------
   float slot[NV + 1];
@@ -270,6 +303,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   });
   const float yv = (v < n) ? slot[NV] * my_inv : 0.f;  // L y = g
   lsync();
+  C1_MARK(2);
 
   // ---- J = L^-T: lane v solves L x = e_v (column v of L^-1 = row v of J) -----------------
   static_for<0, NV>([&](auto C) {
@@ -299,6 +333,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     }
   });
 
+  C1_MARK(3);
   // ---- unconstrained minimiser x = -J y ----------------------------------------------------
   sh.vbuf[v] = yv;
   lsync();
@@ -514,6 +549,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     }
   }
 
+  C1_MARK(4);
   // ---- scatter (q_soln layout 12 k + 3 leg + axis, swing -> 0) staged in LDS, coalesced out
   const bool ok = (status == CMPC_OK);
   for (int t = v; t < 12 * N; t += 64) sh.P[t] = 0.f;
@@ -526,6 +562,15 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     st_out[0] = (uint8_t)status;
     if (it_out) it_out[0] = iters;
   }
+#ifdef CMPC_PHASE_PROF
+  C1_MARK(5);
+  if (v == 0) {
+    ph[6] = 1;
+    ph[7] = (unsigned long long)iters;
+#pragma unroll
+    for (int i = 0; i < 8; i++) atomicAdd(&g_c1_phase[i], ph[i]);
+  }
+#endif
 }
 
 }  // namespace
@@ -554,3 +599,14 @@ hipError_t launch_class1(const float* d_recs, int batch, const KParams& P, float
 }
 
 }  // namespace cmpc
+
+#ifdef CMPC_PHASE_PROF
+// cycles per stage summed over solved class-1 instances: prep, condensation, Cholesky, J,
+// active set (incl. x = -J y), scatter; [6] instances, [7] active-set iterations. Resets.
+extern "C" int cmpc_debug_phase_read(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c1_phase), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -1;
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_c1_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -1,9 +1,11 @@
-// cmpc_class2.hip — size classes 2a / 2b: fused condensation + friction-cone QP for instances
-// with 64 < n <= 96 (class 2a: random contact tables at N = 10, trot at N = 11..16) and
-// 96 < n <= 128 (class 2b: trot at N = 17..21) reduced force variables, one 128-lane workgroup
-// (two wavefronts) per instance, over the previous class's overflow list. The row width NV is a
-// template parameter: a 96-wide row fits the 256-VGPR budget of a 2-wave/SIMD kernel without
-// spilling, a 128-wide one does not, so most class-2 work at N = 10 runs in the narrow kernel.
+// cmpc_class2.h — size class 2 (template over the row width NV): fused condensation + friction-cone QP for instances
+// with 64 < n <= NV reduced force variables (NV = 80, 96, 128: random contact tables at N = 10,
+// trot at N = 11..16, trot at N = 17..21), one 128-lane workgroup (two wavefronts) per
+// instance, over the previous class's overflow list. The row width NV is a
+// template parameter: rows of 80 / 96 fit the 256-VGPR budget of a 2-wave/SIMD kernel without
+// spilling, a 128-wide one does not, so class-2 work at N = 10 (n <= 78 in 99 % of the
+// random-contact instances) runs in the narrowest kernel. One translation unit per width
+// (cmpc_class2_w*.hip) so the unrolled kernels compile in parallel.
 //
 // Same computation as cmpc_class1.hip — one call of the reference's solve_mpc()
 // (be2r_cmpc_unitree/src/controllers/convexMPC/SolverMPC.cpp:566-982) — with the same mapping:
@@ -18,6 +20,7 @@
 //     the implicit R of class 1 would need a cross-wave reduction per active constraint;
 //   * cross-wave scalars (|x| max, |d|^2, the dual step) go through a few LDS words.
 // Everything is fp32 (the reference condenses in fp32: common_types.h:14).
+#pragma once
 #include "cmpc_common.h"
 
 #ifndef CMPC_W2_WAVES_PER_EU
@@ -45,12 +48,12 @@ struct Geo {
 // R (upper triangular, q x q) packed by columns: R[i][j] at rcol(j) + i, i <= j
 __device__ __forceinline__ int rcol(int j) { return (j * (j + 1)) >> 1; }
 
-constexpr int OFF_TRAJ = 0;
-constexpr int OFF_E = 12 * MAXN;
+constexpr int OFF_E = 0;
 constexpr int OFF_ZE = OFF_E + 16 * MAXN;
-static_assert(OFF_ZE + 16 * MAXN <= Geo<96>::PSZ, "prep scratch must fit in P");
+constexpr int OFF_REC = OFF_ZE + 16 * MAXN;  // LDS copy of the instance record (16-B aligned)
+static_assert(OFF_REC + CMPC_REC_WORDS(MAXN) <= Geo<80>::PSZ, "prep scratch must fit in P");
 
-// per-thread arrays are NT long (lanes v >= NV write them too); 25 KB (NV = 96) / 40 KB (128)
+// per-thread arrays are NT long (lanes v >= NV write them too); 19 / 25 / 40 KB (NV = 80 / 96 / 128)
 template <int NV>
 struct SharedC2 {
   float P[Geo<NV>::PSZ];
@@ -102,10 +105,20 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
   const int lane = v & 63;
   const int wave = __builtin_amdgcn_readfirstlane(v >> 6);  // wave-uniform: scalar branches
   const int N = P.N;
+  // ---- stage the record in LDS: one 16-B load per lane, so the whole prep waits on a single
+  // HBM round trip (record words are a multiple of 4, records 16-B aligned)
+  {
+    const float4* src = reinterpret_cast<const float4*>(rec);
+    float4* dst = reinterpret_cast<float4*>(&sh.P[OFF_REC]);
+    for (int t = v; t < (P.rec_words >> 2); t += NT) dst[t] = src[t];
+  }
+  bar();
+  const float* srec = &sh.P[OFF_REC];
   // ---- stance table + elimination (SolverMPC.cpp:869-894): both wavefronts compact it (same
   // result), wavefront 0 stores it
-  const unsigned char* gait = reinterpret_cast<const unsigned char*>(rec + CMPC_REC_HDR + 12 * N);
+  const unsigned char* gait = reinterpret_cast<const unsigned char*>(srec + CMPC_REC_HDR + 12 * N);
   int nfs = 0;
+  unsigned long long msk0 = 0ull, msk1 = 0ull;  // stance ballots of foot-steps 0..63, 64..127
   for (int c0 = 0; c0 < 4 * N; c0 += 64) {
     const int t = c0 + lane;
     float ub = 0.f;
@@ -116,6 +129,7 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
       if (wave == 0) sh.stance[t] = f ? 1 : 0;
     }
     const unsigned long long m = __ballot(f);
+    if (c0 == 0) msk0 = m; else msk1 = m;
     const int pre = __popcll(m & ((1ull << lane) - 1ull));
     if (f && wave == 0) {
       sh.sfs[nfs + pre] = t;
@@ -125,7 +139,7 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
   }
   const int n = 3 * nfs;
   if (n > NV) {  // hand the instance to the next (wider) class
-    if (v == 0) ovf_list[atomicAdd(ovf_count, 1)] = inst;
+    if (v == 0 && ovf_list) ovf_list[atomicAdd(ovf_count, 1)] = inst;
     return;
   }
   bar();
@@ -138,21 +152,21 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
     }
     sh.varblk[v] = (unsigned char)kb;
     sh.varcol[v] = (unsigned char)kc;
-    if (v <= N) {
-      int c = 0;
-      for (int s = 0; s < nfs; s++) c += (sh.sfs[s] < 4 * v) ? 1 : 0;
-      sh.blkbase[v] = 3 * c;
+    if (v <= N) {  // stance foot-steps before step v: popcounts of the ballots
+      const int b0 = 4 * v, b1 = 4 * v - 64;
+      const unsigned long long lo = (b0 >= 64) ? msk0 : (msk0 & ((1ull << b0) - 1ull));
+      const unsigned long long hi = (b1 <= 0) ? 0ull : (msk1 & ((1ull << b1) - 1ull));
+      sh.blkbase[v] = 3 * (__popcll(lo) + __popcll(hi));
     }
     for (int t = v; t < 6 * nfs; t += NT) sh.cflag[t] = 0;
-    for (int t = v; t < 12 * N; t += NT) sh.P[OFF_TRAJ + t] = rec[CMPC_REC_HDR + t];
   }
   Model md;
-  make_model(rec, P.dt, md);
-  make_bdt<NT>(rec, md, v, sh.BdtT);
+  make_model(srec, P.dt, md);
+  make_bdt<NT>(srec, md, v, sh.BdtT);
   bar();
   if (v < N) {
     float e[13];
-    state_error(rec, md, v, &sh.P[OFF_TRAJ + 12 * v], e);
+    state_error(srec, md, v, srec + CMPC_REC_HDR + 12 * v, e);
 #pragma unroll
     for (int j = 0; j < 13; j++) sh.P[OFF_E + 16 * v + j] = e[j];
   }
@@ -587,8 +601,9 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
 
 }  // namespace
 
-// One workgroup per entry of the previous class's overflow list; the grid is sized for the worst
-// case (the list length is only known on the device) and surplus workgroups exit at once.
+// One workgroup per entry of the class's list; the grid is sized for the worst case (the list
+// length is only known on the device) and surplus workgroups exit at once. (A persistent grid
+// looping over the list was measured slower: it serialises the long class-2 solves.)
 template <int NV>
 __global__ __launch_bounds__(NT, CMPC_W2_WAVES_PER_EU) void cmpc_solve_c2_kernel(
     const float* __restrict__ recs, KParams P, float* __restrict__ forces,
@@ -602,19 +617,13 @@ __global__ __launch_bounds__(NT, CMPC_W2_WAVES_PER_EU) void cmpc_solve_c2_kernel
                status + inst, iters ? iters + inst : nullptr, ovf_list, ovf_count, inst);
 }
 
-hipError_t launch_class2(int width, const float* d_recs, int batch, const KParams& P,
-                         float* d_forces, uint8_t* d_status, int32_t* d_iters, const int* in_list,
-                         const int* in_count, int* ovf_list, int* ovf_count, int grid,
-                         hipStream_t stream) {
-  (void)batch;
-  if (width == 96)
-    hipLaunchKernelGGL(cmpc_solve_c2_kernel<96>, dim3(grid), dim3(NT), 0, stream, d_recs, P,
-                       d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
-  else if (width == 128)
-    hipLaunchKernelGGL(cmpc_solve_c2_kernel<128>, dim3(grid), dim3(NT), 0, stream, d_recs, P,
-                       d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
-  else
-    return hipErrorInvalidValue;
+template <int NV>
+hipError_t launch_class2_impl(const float* d_recs, const KParams& P, float* d_forces,
+                              uint8_t* d_status, int32_t* d_iters, const int* in_list,
+                              const int* in_count, int* ovf_list, int* ovf_count, int grid,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(cmpc_solve_c2_kernel<NV>, dim3(grid), dim3(NT), 0, stream, d_recs, P, d_forces,
+                     d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
   return hipGetLastError();
 }
 

@@ -20,26 +20,53 @@ struct KParams {
   int pad;
 };
 
+// Kernel-side copy of cmpc_loco_params + the handle's horizon / record stride.
+struct LocoParams {
+  float dt;
+  int iters_between_mpc;
+  float x_drag_gain;
+  int horizon;
+  int rec_words;
+};
+
 // Scratch ints needed by launch_solve for max_batch instances.
-inline size_t work_ints(int max_batch) { return 4 + 3 * (size_t)max_batch; }
+// d_work: [0] instances with n > 64, [1..4] lengths of the class lists (rows of 80, 96, 128,
+// general), [8 ..) the four lists of max_batch entries each
+inline size_t work_ints(int max_batch) { return 8 + 4 * (size_t)max_batch; }
+// Side streams and events of one handle: the wider size classes run concurrently with class 1
+// (they are latency-bound: few instances, long serial solves). Two side streams: with the
+// handle's own stream that is three of the four hardware queues a process gets by default
+// (GPU_MAX_HW_QUEUES), so no side stream shares a queue with class 1.
+constexpr int kSideStreams = 2;
+struct LaunchCtx {
+  hipStream_t side[kSideStreams] = {nullptr, nullptr};
+  hipEvent_t fork = nullptr;
+  hipEvent_t join[kSideStreams] = {nullptr, nullptr};
+};
 // Workgroups of the general class (persistent over its overflow list) and its global slabs.
 inline int classg_grid(int max_batch) { return max_batch < 512 ? max_batch : 512; }
 size_t classg_scratch_floats(int horizon, int grid);
 
-// ev (optional): 3 events recorded around the size-class launches
-// (ev[0] before class 1, ev[1] between class 1 and the wider classes, ev[2] after them).
+// ev (optional): 3 events recorded on `stream`: ev[0] before class 1, ev[1] after it, ev[2]
+// after the wider classes (side streams) have joined.
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
-                        float* d_gscratch, hipStream_t stream, hipEvent_t* ev = nullptr);
+                        float* d_gscratch, hipStream_t stream, const LaunchCtx& ctx,
+                        hipEvent_t* ev = nullptr);
 // per-class launchers (cmpc_class1.hip, cmpc_class2.hip, cmpc_classg.hip)
 hipError_t launch_class1(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
-// width: row width of the 2-wavefront class, 96 (class 2a) or 128 (class 2b)
-hipError_t launch_class2(int width, const float* d_recs, int batch, const KParams& P,
-                         float* d_forces, uint8_t* d_status, int32_t* d_iters, const int* in_list,
-                         const int* in_count, int* ovf_list, int* ovf_count, int grid,
-                         hipStream_t stream);
+// 2-wavefront classes by row width (cmpc_class2_w{80,96,128}.hip)
+#define CMPC_DECL_CLASS2(W)                                                                        \
+  hipError_t launch_class2_w##W(const float* d_recs, const KParams& P, float* d_forces,           \
+                                uint8_t* d_status, int32_t* d_iters, const int* in_list,          \
+                                const int* in_count, int* ovf_list, int* ovf_count, int grid,     \
+                                hipStream_t stream);
+CMPC_DECL_CLASS2(80)
+CMPC_DECL_CLASS2(96)
+CMPC_DECL_CLASS2(128)
+#undef CMPC_DECL_CLASS2
 hipError_t launch_classg(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          float* scratch, int grid, hipStream_t stream);
@@ -52,6 +79,9 @@ constexpr int kGaussTaps = 2 * kGaussR7 + 1 + 2 * kGaussR27 + 1;
 hipError_t launch_estimate(float* d_est, const float* d_logs, const float* d_fext3,
                            const float* d_time, float sim_time, float* d_records, int rec_words,
                            float* d_fext6, const float* d_gauss, int batch, hipStream_t stream);
+// batched input assembly (cmpc_assemble.hip): one control tick per instance
+hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, uint8_t* d_due,
+                           int batch, hipStream_t stream);
 // parity hook: full (nothing eliminated) qH [12N x 12N] / qg [12N] per instance
 hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
                            float* scratch, int grid, hipStream_t stream);

@@ -1,47 +1,105 @@
-// cmpc_launch.hip — orchestration of the size classes for one batch solve (host code).
-//   class 1 (cmpc_class1.hip): every instance, one wavefront each; n > 64  -> list 1
-//   class 2a (cmpc_class2.hip, rows of 96): one 128-lane workgroup per list-1 entry; n > 96 -> list 2
-//   class 2b (cmpc_class2.hip, rows of 128): one 128-lane workgroup per list-2 entry; n > 128 -> list 3
-//   class G (cmpc_classg.hip): persistent 256-lane workgroups over list 3 (any n)
+// cmpc_launch.hip — orchestration of the size classes for one batch solve.
+//   classify (this file): n = 3 x stance foot-steps per instance (SolverMPC.cpp:869-894), the
+//     instances with n > 64 appended to the list of their class;
+//   class 1 (cmpc_class1.hip): every instance, one wavefront each; exits when n > 64;
+//   class 2 (cmpc_class2.h), 128-lane workgroups, rows of 80 / 96 / 128, and class G
+//     (cmpc_classg.hip, any n): each over its own list, on two side streams forked after
+//     classify (rows of 80 on one; 96, 128, G on the other), so they run concurrently with
+//     class 1 (they are latency-bound: few, long solves).
 #include "cmpc_kernels.h"
 
 namespace cmpc {
 
+namespace {
+
+// one thread per instance; wave-aggregated appends to the class lists
+__global__ __launch_bounds__(256) void cmpc_classify_kernel(const float* __restrict__ recs, int batch,
+                                                            KParams P, int* __restrict__ cnt,
+                                                            int* __restrict__ lists, int max_batch) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int cls = -1;
+  if (i < batch) {
+    const uint32_t* g =
+        reinterpret_cast<const uint32_t*>(recs + (size_t)i * P.rec_words + CMPC_REC_GAIT(P.N));
+    int nfs = 0;
+    for (int k = 0; k < P.N; k++) {
+      const uint32_t w = g[k];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        // eliminated iff |gait * f_max| < 0.01, exactly as the solver kernels test it
+        const float ub = (float)((w >> (8 * j)) & 0xffu) * P.f_max;
+        nfs += (ub < 0.01f && ub > -0.01f) ? 0 : 1;
+      }
+    }
+    const int n = 3 * nfs;
+    cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : 3;
+  }
+  const unsigned long long any = __ballot(cls >= 0);
+  if (any == 0ull) return;
+  if (lane == 0) atomicAdd(&cnt[0], __popcll(any));
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const unsigned long long m = __ballot(cls == c);
+    if (m == 0ull) continue;
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&cnt[1 + c], __popcll(m));
+    base = __shfl(base, leader);
+    if (cls == c) lists[(size_t)c * max_batch + base + __popcll(m & ((1ull << lane) - 1ull))] = i;
+  }
+}
+
+}  // namespace
+
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
-                        float* d_gscratch, hipStream_t stream, hipEvent_t* ev) {
-  // d_work layout: [0..2] counts of lists 1..3, [4 ..) list 1, then list 2, then list 3
-  int* cnt1 = d_work;
-  int* cnt2 = d_work + 1;
-  int* cnt3 = d_work + 2;
-  int* list1 = d_work + 4;
-  int* list2 = d_work + 4 + max_batch;
-  int* list3 = d_work + 4 + 2 * (size_t)max_batch;
-  hipError_t e = hipMemsetAsync(d_work, 0, 4 * sizeof(int), stream);
+                        float* d_gscratch, hipStream_t stream, const LaunchCtx& ctx,
+                        hipEvent_t* ev) {
+  int* cnt = d_work;
+  int* list[4];
+  for (int j = 0; j < 4; j++) list[j] = d_work + 8 + (size_t)j * max_batch;
+  hipError_t e = hipMemsetAsync(d_work, 0, 8 * sizeof(int), stream);
   if (e != hipSuccess) return e;
   if (batch <= 0) return hipSuccess;
+  const int n_max = 12 * P.N;  // a class no instance of this horizon can reach is not launched
+  const bool wide[4] = {n_max > 64, n_max > 80, n_max > 96, n_max > 128};
+  if (wide[0]) {
+    hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_recs,
+                       batch, P, cnt, d_work + 8, max_batch);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
+    for (int s = 0; s < kSideStreams; s++)
+      if ((e = hipStreamWaitEvent(ctx.side[s], ctx.fork, 0)) != hipSuccess) return e;
+    // one workgroup per possible list entry (the lengths are only known on the device);
+    // surplus workgroups exit after one load
+    if ((e = launch_class2_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], nullptr,
+                               nullptr, batch, ctx.side[0])) != hipSuccess)
+      return e;
+    if (wide[1] && (e = launch_class2_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2],
+                                          nullptr, nullptr, batch, ctx.side[1])) != hipSuccess)
+      return e;
+    if (wide[2] && (e = launch_class2_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
+                                           nullptr, nullptr, batch, ctx.side[1])) != hipSuccess)
+      return e;
+    if (wide[3] && (e = launch_classg(d_recs, batch, P, d_forces, d_status, d_iters, list[3],
+                                      &cnt[4], d_gscratch, classg_grid(max_batch),
+                                      ctx.side[1])) != hipSuccess)
+      return e;
+  }
   if (ev) (void)hipEventRecord(ev[0], stream);
-  e = launch_class1(d_recs, batch, P, d_forces, d_status, d_iters, nullptr, nullptr, list1, cnt1,
-                    batch, stream);
+  e = launch_class1(d_recs, batch, P, d_forces, d_status, d_iters, nullptr, nullptr, nullptr,
+                    nullptr, batch, stream);
   if (e != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
-  if (12 * P.N > 64) {
-    // one workgroup per possible list-1 entry; surplus workgroups exit after one load
-    e = launch_class2(96, d_recs, batch, P, d_forces, d_status, d_iters, list1, cnt1, list2, cnt2,
-                      batch, stream);
-    if (e != hipSuccess) return e;
-  }
-  if (12 * P.N > 96) {
-    e = launch_class2(128, d_recs, batch, P, d_forces, d_status, d_iters, list2, cnt2, list3, cnt3,
-                      batch, stream);
-    if (e != hipSuccess) return e;
-  }
-  if (12 * P.N > 128) {
-    e = launch_classg(d_recs, batch, P, d_forces, d_status, d_iters, list3, cnt3, d_gscratch,
-                      classg_grid(max_batch), stream);
+  if (wide[0]) {
+    for (int s = 0; s < kSideStreams; s++) {
+      if ((e = hipEventRecord(ctx.join[s], ctx.side[s])) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(stream, ctx.join[s], 0)) != hipSuccess) return e;
+    }
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
-  return e;
+  return hipSuccess;
 }
 
 }  // namespace cmpc

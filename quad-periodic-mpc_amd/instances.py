@@ -146,3 +146,82 @@ def make_logs(records: np.ndarray, seed: int = BASE_SEED + 6) -> np.ndarray:
                   2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], -1)
     lg[:, LOG_ROT:LOG_ROT + 9] = R
     return lg
+
+
+# OffsetDurationGait tables of the controller (ConvexMPCLocomotion.cpp:41-51, gait_period P;
+# Vec4<int> of doubles truncates): name -> (offsets, durations, cmpc_gait number)
+def loco_gaits(P: int = 18):
+    return {
+        "trotting": ((0, int(P / 2.0), int(P / 2.0), 0), (int(P / 2.0),) * 4, 9),
+        "bounding": ((5, 5, 0, 0), (4, 4, 4, 4), 1),
+        "pronking": ((0, 0, 0, 0), (8, 8, 8, 8), 2),
+        "galloping": ((0, 2, 7, 9), (4, 4, 4, 4), 6),
+        "standing": ((0, 0, 0, 0), (P, P, P, P), 4),
+        "walking": ((int(2 * P / 4.0), 0, int(P / 4.0), int(3 * P / 4.0)), (int(0.75 * P),) * 4, 10),
+        "pacing": ((5, 0, 5, 0), (5, 5, 5, 5), 8),  # gait 8: rpy_comp[0] off (:230)
+    }
+
+
+def make_loco_states(batch: int, seed: int = BASE_SEED + 11, P: int = 18, first_run_frac: float = 0.1,
+                     gaits=("trotting", "trotting", "trotting", "bounding", "pronking", "galloping",
+                            "standing", "walking", "pacing"), omni_frac: float = 0.1) -> np.ndarray:
+    """Locomotion-controller states [batch, LOCO_WORDS] (include/cmpc_solver.h CMPC_LOCO_*):
+    A1-like body states, world foot positions around the nominal stance, stick commands, a
+    random gait from ``gaits`` at a random iteration counter, and warm integrator states."""
+    from .records import (LOCO_CMD, LOCO_COUNTER, LOCO_FIRST, LOCO_FLAGS, LOCO_GAIT, LOCO_HEIGHT,
+                          LOCO_OMNI, LOCO_PFOOT, LOCO_POS, LOCO_PRONK, LOCO_Q, LOCO_RPY,
+                          LOCO_RPYINT, LOCO_STAND, LOCO_STANDING, LOCO_VDES, LOCO_VW, LOCO_WORDS,
+                          LOCO_WPD, LOCO_WW, LOCO_XCI, LOCO_ZGT)
+    g = np.random.Generator(np.random.Philox(seed))
+    B = batch
+    s = np.zeros((B, LOCO_WORDS), np.float32)
+    roll = np.clip(g.normal(0, 0.05, B), -0.3, 0.3)
+    pitch = np.clip(g.normal(0, 0.05, B), -0.3, 0.3)
+    yaw = g.uniform(-np.pi, np.pi, B)
+    pos = np.stack([g.uniform(-1, 1, B), g.uniform(-1, 1, B), 0.29 + g.normal(0, 0.02, B)], -1)
+    s[:, LOCO_POS:LOCO_POS + 3] = pos
+    s[:, LOCO_ZGT] = pos[:, 2] + g.normal(0, 0.005, B)
+    s[:, LOCO_Q:LOCO_Q + 4] = euler_zyx_to_quat(roll, pitch, yaw)
+    s[:, LOCO_RPY:LOCO_RPY + 3] = np.stack([roll, pitch, yaw], -1)
+    vw = np.stack([g.uniform(-0.7, 0.7, B), g.uniform(-0.4, 0.4, B), g.normal(0, 0.05, B)], -1)
+    vw[g.random(B) < 0.2, 0] *= 0.2     # some slow instances: the |v| thresholds of :218-222
+    s[:, LOCO_VW:LOCO_VW + 3] = vw
+    s[:, LOCO_WW:LOCO_WW + 3] = g.normal(0, 0.3, (B, 3))
+    cy, sy = np.cos(yaw)[:, None], np.sin(yaw)[:, None]
+    bx = _HIP_X[None, :] + g.normal(0, 0.03, (B, 4))
+    by = _HIP_Y[None, :] + g.normal(0, 0.03, (B, 4))
+    pf = np.stack([pos[:, 0:1] + cy * bx - sy * by, pos[:, 1:2] + sy * bx + cy * by,
+                   g.normal(0, 0.01, (B, 4))], -1)          # [B, leg, axis]
+    s[:, LOCO_PFOOT:LOCO_PFOOT + 12] = pf.reshape(B, 12)
+    s[:, LOCO_CMD] = g.uniform(-0.7, 0.7, B)
+    s[:, LOCO_CMD + 1] = g.uniform(-0.4, 0.4, B)
+    s[:, LOCO_CMD + 2] = g.uniform(-2.5, 2.5, B)
+    s[:, LOCO_HEIGHT] = 0.29
+    s[:, LOCO_VDES] = s[:, LOCO_CMD] * g.uniform(0, 1, B)
+    s[:, LOCO_VDES + 1] = s[:, LOCO_CMD + 1] * g.uniform(0, 1, B)
+    s[:, LOCO_WPD:LOCO_WPD + 2] = pos[:, :2] + g.uniform(-0.2, 0.2, (B, 2))
+    s[:, LOCO_RPYINT:LOCO_RPYINT + 2] = g.uniform(-0.3, 0.3, (B, 2))
+    s[:, LOCO_XCI] = g.uniform(-0.5, 0.5, B)
+    tab = loco_gaits(P)
+    names = [gaits[k] for k in g.integers(0, len(gaits), B)]
+    ints = np.zeros((B, 10), np.int32)
+    flags = np.zeros(B, np.uint32)
+    for b, nm in enumerate(names):
+        off, dur, num = tab[nm]
+        ints[b, 0] = P
+        ints[b, 1:5] = off
+        ints[b, 5:9] = dur
+        if num == 4:
+            flags[b] |= LOCO_STANDING
+        if num == 8:
+            flags[b] |= LOCO_PRONK
+    ints[:, 9] = g.integers(0, 100000, B)                   # iterationCounter
+    flags[g.random(B) < omni_frac] |= LOCO_OMNI
+    flags[g.random(B) < first_run_frac] |= LOCO_FIRST
+    s[:, LOCO_GAIT:LOCO_GAIT + 9] = ints[:, :9].view(np.float32)
+    s[:, LOCO_COUNTER] = ints[:, 9].view(np.float32)
+    s[:, LOCO_FLAGS] = flags.view(np.float32)
+    s[:, LOCO_STAND] = pos[:, 0]
+    s[:, LOCO_STAND + 1] = pos[:, 1]
+    s[:, LOCO_STAND + 2] = yaw
+    return s

@@ -31,6 +31,23 @@ EST_F, EST_T, EST_COUNT, EST_HEAD, EST_FEST3, EST_PARAMS = 0, 400, 800, 801, 802
 EST_WORDS = 816
 
 STATUS_NAMES = {0: "ok", 1: "max_iter", 2: "infeasible", 3: "not_pd", 4: "bad_input"}
+# locomotion-controller state for batched input assembly (include/cmpc_solver.h CMPC_LOCO_*)
+LOCO_POS, LOCO_ZGT, LOCO_Q, LOCO_RPY, LOCO_VW, LOCO_WW, LOCO_PFOOT = 0, 3, 4, 8, 11, 14, 17
+LOCO_CMD, LOCO_HEIGHT, LOCO_VDES, LOCO_WPD, LOCO_RPYINT, LOCO_XCI = 29, 32, 33, 35, 37, 39
+LOCO_COUNTER, LOCO_GAIT, LOCO_FLAGS, LOCO_STAND = 40, 41, 50, 51
+LOCO_WORDS = 56
+LOCO_OMNI, LOCO_STANDING, LOCO_PRONK, LOCO_FIRST = 1, 2, 4, 8
+
+
+class LocoParams(ctypes.Structure):
+    """cmpc_loco_params (include/cmpc_solver.h)."""
+    _fields_ = [("dt", ctypes.c_float), ("iters_between_mpc", ctypes.c_int),
+                ("x_drag_gain", ctypes.c_float), ("pad", ctypes.c_int)]
+
+
+def make_loco_params(dt: float = 0.002, iters_between_mpc: int = 13,
+                     x_drag_gain: float = 0.0) -> LocoParams:
+    return LocoParams(dt, iters_between_mpc, x_drag_gain, 0)
 
 
 def record_words(horizon: int) -> int:

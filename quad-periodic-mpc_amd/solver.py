@@ -19,7 +19,7 @@ import os
 
 import numpy as np
 
-from .records import CmpcParams, make_params, record_words
+from .records import CmpcParams, LocoParams, make_params, record_words
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CMPC_LIB", os.path.join(PKG, "libcmpc_hip.so"))
@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
     "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
     "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing", "cmpc_batch_estimate",
+    "cmpc_batch_assemble",
 )
 
 _lib = None
@@ -83,6 +84,9 @@ def load_library(path: str = LIB_PATH):
     lib.cmpc_batch_estimate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    lib.cmpc_batch_assemble.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.POINTER(LocoParams), ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_int]
     _lib = lib
     return lib
 
@@ -241,6 +245,18 @@ class BatchSolver:
         _check(self.lib.cmpc_batch_estimate(self._h, _ptr(est_state), _ptr(logs), _ptr(fext3),
                                             _ptr(times), float(sim_time), _ptr(records),
                                             _ptr(fext6), int(batch)), "cmpc_batch_estimate")
+
+    def assemble(self, loco, loco_params: LocoParams, records, due, batch: int | None = None) -> None:
+        """One control tick of every instance's locomotion controller on device
+        (``cmpc_batch_assemble``): updates ``loco`` [B, LOCO_WORDS] and, where an MPC step is
+        due, writes that instance's solve record into ``records`` and ``due[i] = 1``."""
+        if batch is None:
+            batch = loco.shape[0]
+        if hasattr(records, "shape"):
+            assert records.shape[-1] == self.record_words, "record stride mismatch"
+        _check(self.lib.cmpc_batch_assemble(self._h, _ptr(loco), ctypes.byref(loco_params),
+                                            _ptr(records), _ptr(due), int(batch)),
+               "cmpc_batch_assemble")
 
     def enable_timing(self, steps: int) -> None:
         """Record HIP events around each size-class launch of the next ``steps`` solves."""
