@@ -291,10 +291,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 #pragma unroll
       for (int c = c0; c < NV; c += 4) {
         const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
-        slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
-        slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
-        slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
-        slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+        axpy4(a, r4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
         CMPC_SWEEP_FENCE(c);
       }
       slot[NV] = fmaf(a, sh.gbuf[k], slot[NV]);
@@ -322,10 +319,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 #pragma unroll
       for (int c = c0; c < NV; c += 4) {
         const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
-        slot[c + 0] = fmaf(a, r4.x, slot[c + 0]);
-        slot[c + 1] = fmaf(a, r4.y, slot[c + 1]);
-        slot[c + 2] = fmaf(a, r4.z, slot[c + 2]);
-        slot[c + 3] = fmaf(a, r4.w, slot[c + 3]);
+        axpy4(a, r4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
         CMPC_SWEEP_FENCE(c);
       }
       slot[k] = xk;
@@ -337,17 +331,14 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   // ---- unconstrained minimiser x = -J y ----------------------------------------------------
   sh.vbuf[v] = yv;
   lsync();
-  float xv = 0.f;
+  f2v xacc = {0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < NV; c += 4) {
     const float4 y4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-    xv = fmaf(slot[c + 0], y4.x, xv);
-    xv = fmaf(slot[c + 1], y4.y, xv);
-    xv = fmaf(slot[c + 2], y4.z, xv);
-    xv = fmaf(slot[c + 3], y4.w, xv);
+    dot4(xacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], y4);
     CMPC_SWEEP_FENCE(c);
   }
-  xv = (v < n) ? -xv : 0.f;
+  float xv = (v < n) ? -(xacc.x + xacc.y) : 0.f;
   lsync();
 
   // ---- Goldfarb-Idnani dual active set on the friction pyramids -----------------------------
@@ -414,17 +405,15 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       sh.vbuf[v] = dm;
       lsync();
       // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+, dn = |d|^2
-      float zv = 0.f, zn = 0.f;
+      f2v zacc = {0.f, 0.f}, nacc = {0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < NV; c += 4) {
         const float4 m4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-        zv = fmaf(slot[c + 0], m4.x, zv);
-        zv = fmaf(slot[c + 1], m4.y, zv);
-        zv = fmaf(slot[c + 2], m4.z, zv);
-        zv = fmaf(slot[c + 3], m4.w, zv);
-        zn += m4.x * m4.x + m4.y * m4.y + m4.z * m4.z + m4.w * m4.w;
+        dot4(zacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], m4);
+        dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
         CMPC_SWEEP_FENCE(c);
       }
+      const float zv = zacc.x + zacc.y, zn = nacc.x + nacc.y;
       const float dn = wave_sum((v < n) ? dv * dv : 0.f);
       // r = R^-1 d1: back substitution over the packed columns of R (lane i ends with r_i)
       float acc = dv, r_reg = 0.f;
@@ -506,27 +495,21 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       lsync();
       // J <- J (I - beta w w'): tw = J_v . w, J_v -= beta tw w  (no-op on a drop: beta = 0)
       {
-        float tw = 0.f;
+        f2v tacc = {0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < NV; c += 4) {
           const float4 w4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-          tw = fmaf(slot[c + 0], w4.x, tw);
-          tw = fmaf(slot[c + 1], w4.y, tw);
-          tw = fmaf(slot[c + 2], w4.z, tw);
-          tw = fmaf(slot[c + 3], w4.w, tw);
+          dot4(tacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], w4);
           CMPC_SWEEP_FENCE(c);
         }
-        const float bt = -beta * tw;
+        const float bt = -beta * (tacc.x + tacc.y);
         // re-read w from LDS: without this point the compiler keeps all NV values of the first
         // sweep's loads live for the second (a whole row of extra VGPRs)
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int c = 0; c < NV; c += 4) {
           const float4 w4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-          slot[c + 0] = fmaf(bt, w4.x, slot[c + 0]);
-          slot[c + 1] = fmaf(bt, w4.y, slot[c + 1]);
-          slot[c + 2] = fmaf(bt, w4.z, slot[c + 2]);
-          slot[c + 3] = fmaf(bt, w4.w, slot[c + 3]);
+          axpy4(bt, w4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
           CMPC_SWEEP_FENCE(c);
         }
       }

@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name: str) -> str:
-    return name.split("(")[0].replace("void ", "").strip()
+    return name.replace("(anonymous namespace)", "anon").split("(")[0].replace("void ", "").strip()
 
 
 def counters(path):
