@@ -217,6 +217,17 @@ CMPC_EXTERNC int cmpc_batch_estimate(cmpc_batch* h, float* d_est, const float* d
  * past its P-row table. Asynchronous on the handle's stream. */
 CMPC_EXTERNC int cmpc_batch_assemble(cmpc_batch* h, float* d_loco, const cmpc_loco_params* lp,
                                      float* d_records, uint8_t* d_due, int batch);
+/* Closes the loop of a batched MPC simulator: for every instance with d_due[i] != 0 (all when
+ * d_due is NULL), advances the single-rigid-body state of its record by one MPC step with its
+ * own prediction model and the step-0 forces of the solve (d_forces[i][0..11]), plus an
+ * optional disturbance d_xi6[i] = [tau(3), f(3)] through Qdt (Q_ct of SolverMPC.cpp:607-615):
+ *   x+ = Adt x0 + Bdt u0 + Qdt xi   (the discretisation of c2qp, SolverMPC.cpp:96-146)
+ * and writes rpy / p / w / v (+ the quaternion, z_groundtruth = p_z) into d_loco[i]; the feet
+ * move with the body in x, y (footstep relocation is not simulated). The step is the handle's
+ * dt (dtMPC). Asynchronous on the handle's stream. */
+CMPC_EXTERNC int cmpc_batch_rollout(cmpc_batch* h, float* d_loco, const float* d_records,
+                                    const float* d_forces, const float* d_xi6,
+                                    const uint8_t* d_due, int batch);
 /* Measurement hooks: record HIP events around each size-class launch of the next `steps`
  * solves; read back per-launch ms pairs [class1, class2] and class 1's overflow count (the
  * number of instances handed to the 2-wave class in the last solve). Synchronises. */

@@ -212,6 +212,20 @@ extern "C" int cmpc_batch_assemble(cmpc_batch* h, float* d_loco, const cmpc_loco
   return 0;
 }
 
+extern "C" int cmpc_batch_rollout(cmpc_batch* h, float* d_loco, const float* d_records,
+                                  const float* d_forces, const float* d_xi6, const uint8_t* d_due,
+                                  int batch) {
+  if (!h || batch < 0 || batch > h->max_batch || (batch && (!d_loco || !d_records || !d_forces))) {
+    g_last_error = "cmpc_batch_rollout: bad arguments";
+    return -1;
+  }
+  cmpc::LocoParams kp{h->kp.dt, 1, 0.f, h->kp.N, h->kp.rec_words};
+  hipError_t e = cmpc::launch_rollout(d_loco, d_records, d_forces, d_xi6, d_due, kp, h->kp.dt,
+                                      batch, h->stream);
+  if (e != hipSuccess) return fail("launch_rollout", e);
+  return 0;
+}
+
 extern "C" int cmpc_batch_enable_timing(cmpc_batch* h, int steps) {
   if (!h || steps < 0) return -1;
   for (auto e : h->ev) (void)hipEventDestroy(e);

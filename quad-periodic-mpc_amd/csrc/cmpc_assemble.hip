@@ -1,4 +1,7 @@
-// cmpc_assemble.hip — batched on-device MPC input assembly.
+// cmpc_assemble.hip — the batched controller loop around the solver:
+//   * cmpc_assemble_kernel: on-device MPC input assembly (rank 1, below);
+//   * cmpc_rollout_kernel: the single-rigid-body step x+ = Adt x + Bdt u0 + Qdt xi that closes
+//     the loop in a batched MPC simulator (rank 2, at the end of this file).
 //
 // One thread advances one instance's locomotion controller by one control tick, doing exactly
 // the MPC-input side of ConvexMPCLocomotion::run (be2r_cmpc_unitree/src/controllers/convexMPC/
@@ -22,7 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "cmpc_kernels.h"
+#include "cmpc_common.h"
 
 #pragma clang fp contract(off)
 
@@ -186,6 +189,105 @@ __global__ __launch_bounds__(256) void cmpc_assemble_kernel(float* __restrict__ 
   due[i] = mpc ? 1 : 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Rollout: advance each due instance by one MPC step with its own prediction model, the
+// discretised single rigid body of solve_mpc (RobotState::set + ct_ss_mats + c2qp,
+// SolverMPC.cpp:96-146, 260-279, 566-620; cmpc_common.h), driven by the step-0 forces of the
+// solve and an optional disturbance xi (the f_ext layout [tau(3), f(3)] of Q_ct,
+// SolverMPC.cpp:607-615):
+//   x+ = Adt x0 + Bdt u0 + Qdt xi,  Qdt = dt Q + dt^2/2 A Q + dt^3/6 A^2 Q (A^3 = 0),
+// with x0 = [rpy, p, w, v, -9.8] from the record. The new rpy / p / w / v are written back to
+// the controller state (quaternion from ZYX Euler angles, z_groundtruth = p_z). The feet move
+// with the body in x and y (footstep relocation is not simulated: each foot keeps its offset
+// from the body, on the ground). One thread per instance.
+__global__ __launch_bounds__(256) void cmpc_rollout_kernel(float* __restrict__ loco,
+                                                           const float* __restrict__ recs,
+                                                           const float* __restrict__ forces,
+                                                           const float* __restrict__ xi6,
+                                                           const uint8_t* __restrict__ due,
+                                                           LocoParams lp, float dt, int batch) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch || (due && !due[i])) return;
+  const float* rec = recs + (size_t)i * lp.rec_words;
+  const float* u = forces + (size_t)i * 12 * lp.horizon;  // step 0: 12 forces, leg * 3 + axis
+  Model md;
+  make_model(rec, dt, md);
+  float BdtT[12][16];
+#pragma unroll
+  for (int c = 0; c < 12; c++) make_bdt<12>(rec, md, c, BdtT);
+  float x0[13];
+  {
+    const float qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],
+                qz = rec[CMPC_REC_Q + 3];
+    float as = -2.f * (qx * qz - qw * qy);
+    as = fminf(as, 0.99999f);  // quat_to_rpy (SolverMPC.cpp:352-361)
+    x0[0] = atan2f(2.f * (qy * qz + qw * qx), qw * qw - qx * qx - qy * qy + qz * qz);
+    x0[1] = asinf(as);
+    x0[2] = atan2f(2.f * (qx * qy + qw * qz), qw * qw + qx * qx - qy * qy - qz * qz);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      x0[3 + k] = rec[CMPC_REC_P + k];
+      x0[6 + k] = rec[CMPC_REC_W + k];
+      x0[9 + k] = rec[CMPC_REC_V + k];
+    }
+    x0[12] = -9.8f;
+  }
+  float x1[13];
+  n1_mul(md, x0, x1);  // Adt x0 = x0 + N1 x0
+#pragma unroll
+  for (int j = 0; j < 13; j++) x1[j] = x0[j] + x1[j];
+#pragma unroll
+  for (int c = 0; c < 12; c++) {
+    const float uc = u[c];
+#pragma unroll
+    for (int j = 0; j < 13; j++) x1[j] = x1[j] + BdtT[c][j] * uc;
+  }
+  if (xi6) {
+    const float* xi = xi6 + (size_t)i * 6;
+    float y[13], Ay[13], AAy[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) y[j] = (j >= 6 && j < 12) ? xi[j - 6] : 0.f;
+    // A y: rows 0..2 = R^T y[6..8] (n1r = dt R^T), rows 3..5 = y[9..11], row 11 = x_drag y[9]
+#pragma unroll
+    for (int j = 0; j < 13; j++) Ay[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+      Ay[r] = md.R[0 * 3 + r] * y[6] + md.R[1 * 3 + r] * y[7] + md.R[2 * 3 + r] * y[8];
+    Ay[3] = y[9];
+    Ay[4] = y[10];
+    Ay[5] = y[11];
+    Ay[11] = md.xdrag * y[9];
+#pragma unroll
+    for (int j = 0; j < 13; j++) AAy[j] = 0.f;
+    AAy[5] = Ay[11];  // A (A y): rows 3..5 <- (A y)[9..11], rows 0..2 <- R^T (A y)[6..8] = 0
+    const float dt2 = dt * dt * 0.5f, dt3 = dt * dt * dt / 6.f;
+#pragma unroll
+    for (int j = 0; j < 13; j++) x1[j] = x1[j] + (dt * y[j] + dt2 * Ay[j] + dt3 * AAy[j]);
+  }
+  float* s = loco + (size_t)i * CMPC_LOCO_WORDS;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    s[CMPC_LOCO_RPY + k] = x1[k];
+    s[CMPC_LOCO_POS + k] = x1[3 + k];
+    s[CMPC_LOCO_WW + k] = x1[6 + k];
+    s[CMPC_LOCO_VW + k] = x1[9 + k];
+  }
+  s[CMPC_LOCO_ZGT] = x1[5];
+#pragma unroll
+  for (int l = 0; l < 4; l++) {
+    s[CMPC_LOCO_PFOOT + 3 * l + 0] += x1[3] - x0[3];
+    s[CMPC_LOCO_PFOOT + 3 * l + 1] += x1[4] - x0[4];
+  }
+  // ZYX Euler -> quaternion (w, x, y, z)
+  const float cr = cosf(0.5f * x1[0]), sr = sinf(0.5f * x1[0]);
+  const float cp = cosf(0.5f * x1[1]), sp = sinf(0.5f * x1[1]);
+  const float cy = cosf(0.5f * x1[2]), sy = sinf(0.5f * x1[2]);
+  s[CMPC_LOCO_Q + 0] = cr * cp * cy + sr * sp * sy;
+  s[CMPC_LOCO_Q + 1] = sr * cp * cy - cr * sp * sy;
+  s[CMPC_LOCO_Q + 2] = cr * sp * cy + sr * cp * sy;
+  s[CMPC_LOCO_Q + 3] = cr * cp * sy - sr * sp * cy;
+}
+
 }  // namespace
 
 hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, uint8_t* d_due,
@@ -193,6 +295,15 @@ hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, u
   if (batch <= 0) return hipSuccess;
   hipLaunchKernelGGL(cmpc_assemble_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_loco,
                      lp, d_recs, d_due, batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout(float* d_loco, const float* d_recs, const float* d_forces,
+                          const float* d_xi6, const uint8_t* d_due, const LocoParams& lp, float dt,
+                          int batch, hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cmpc_rollout_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_loco,
+                     d_recs, d_forces, d_xi6, d_due, lp, dt, batch);
   return hipGetLastError();
 }
 

@@ -82,6 +82,10 @@ hipError_t launch_estimate(float* d_est, const float* d_logs, const float* d_fex
 // batched input assembly (cmpc_assemble.hip): one control tick per instance
 hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, uint8_t* d_due,
                            int batch, hipStream_t stream);
+// single-rigid-body step of every due instance with its solved step-0 forces (cmpc_assemble.hip)
+hipError_t launch_rollout(float* d_loco, const float* d_recs, const float* d_forces,
+                          const float* d_xi6, const uint8_t* d_due, const LocoParams& lp, float dt,
+                          int batch, hipStream_t stream);
 // parity hook: full (nothing eliminated) qH [12N x 12N] / qg [12N] per instance
 hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
                            float* scratch, int grid, hipStream_t stream);

@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
     "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
     "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing", "cmpc_batch_estimate",
-    "cmpc_batch_assemble",
+    "cmpc_batch_assemble", "cmpc_batch_rollout",
 )
 
 _lib = None
@@ -87,6 +87,9 @@ def load_library(path: str = LIB_PATH):
     lib.cmpc_batch_assemble.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.POINTER(LocoParams), ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_int]
+    lib.cmpc_batch_rollout.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int]
     _lib = lib
     return lib
 
@@ -257,6 +260,14 @@ class BatchSolver:
         _check(self.lib.cmpc_batch_assemble(self._h, _ptr(loco), ctypes.byref(loco_params),
                                             _ptr(records), _ptr(due), int(batch)),
                "cmpc_batch_assemble")
+
+    def rollout(self, loco, records, forces, xi6=None, due=None, batch: int | None = None) -> None:
+        """One single-rigid-body MPC step of every due instance on device
+        (``cmpc_batch_rollout``): x+ = Adt x0 + Bdt u0 (+ Qdt xi) into ``loco``."""
+        if batch is None:
+            batch = loco.shape[0]
+        _check(self.lib.cmpc_batch_rollout(self._h, _ptr(loco), _ptr(records), _ptr(forces),
+                                           _ptr(xi6), _ptr(due), int(batch)), "cmpc_batch_rollout")
 
     def enable_timing(self, steps: int) -> None:
         """Record HIP events around each size-class launch of the next ``steps`` solves."""
