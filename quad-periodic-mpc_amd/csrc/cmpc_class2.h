@@ -26,6 +26,12 @@
 #ifndef CMPC_W2_WAVES_PER_EU
 #define CMPC_W2_WAVES_PER_EU 2
 #endif
+// Rows of 128 do not fit 256 VGPRs. At one wave per SIMD (-DCMPC_W128_WAVES_PER_EU=1) the kernel
+// may use the whole unified register file (299 VGPRs + 43 AGPRs, no scratch), but that was
+// measured slower than two waves per SIMD with scratch spills: 2.05 vs 2.67 M QP/s at N = 20 trot.
+#ifndef CMPC_W128_WAVES_PER_EU
+#define CMPC_W128_WAVES_PER_EU 2
+#endif
 
 namespace cmpc {
 namespace {
@@ -605,7 +611,8 @@ __device__ __forceinline__ void solve_c2(const float* __restrict__ rec, const KP
 // length is only known on the device) and surplus workgroups exit at once. (A persistent grid
 // looping over the list was measured slower: it serialises the long class-2 solves.)
 template <int NV>
-__global__ __launch_bounds__(NT, CMPC_W2_WAVES_PER_EU) void cmpc_solve_c2_kernel(
+__global__ __launch_bounds__(NT, (NV >= 128 ? CMPC_W128_WAVES_PER_EU : CMPC_W2_WAVES_PER_EU)) void
+cmpc_solve_c2_kernel(
     const float* __restrict__ recs, KParams P, float* __restrict__ forces,
     uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
     const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {

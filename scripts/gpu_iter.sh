@@ -15,6 +15,7 @@ step() {  # name, timeout, cmd...
 step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread || exit 1
 step diag 300 python -u scripts/diag_classes.py || exit 1
 step bench 300 python -u bench.py --no-cpu-baseline || exit 1
+step bench_c5 300 python -u bench.py --no-cpu-baseline --config5 --steps 50 || exit 1
 if [ -f quad-periodic-mpc_amd/libcmpc_prof.so ]; then
   step phase 200 python -u scripts/phase_prof.py || exit 1
 fi
