@@ -44,7 +44,7 @@ struct LaunchCtx {
   hipEvent_t join[kSideStreams] = {nullptr, nullptr};
 };
 // Workgroups of the general class (persistent over its overflow list) and its global slabs.
-inline int classg_grid(int max_batch) { return max_batch < 512 ? max_batch : 512; }
+inline int classg_grid(int max_batch) { return max_batch < 2048 ? max_batch : 2048; }
 size_t classg_scratch_floats(int horizon, int grid);
 
 // ev (optional): 3 events recorded on `stream`: ev[0] before class 1, ev[1] after it, ev[2]

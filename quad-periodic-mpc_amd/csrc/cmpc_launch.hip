@@ -4,8 +4,9 @@
 //   class 1 (cmpc_class1.hip): every instance, one wavefront each; exits when n > 64;
 //   class 2 (cmpc_class2.h), 128-lane workgroups, rows of 80 / 96 / 128, and class G
 //     (cmpc_classg.hip, any n): each over its own list, on two side streams forked after
-//     classify (rows of 80 on one; 96, 128, G on the other), so they run concurrently with
-//     class 1 (they are latency-bound: few, long solves).
+//     classify (rows of 80, then G, on one; 96, 128 on the other), so they run concurrently
+//     with class 1 and with each other (at N = 10 they are latency-bound: few, long solves; at
+//     N = 20 the 128-row class and G carry most of the batch).
 #include "cmpc_kernels.h"
 
 namespace cmpc {
@@ -84,7 +85,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       return e;
     if (wide[3] && (e = launch_classg(d_recs, batch, P, d_forces, d_status, d_iters, list[3],
                                       &cnt[4], d_gscratch, classg_grid(max_batch),
-                                      ctx.side[1])) != hipSuccess)
+                                      ctx.side[0])) != hipSuccess)
       return e;
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
