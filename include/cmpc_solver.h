@@ -194,6 +194,22 @@ CMPC_EXTERNC int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int 
  * (row-major) and qg per instance, all variables kept (no swing elimination). */
 CMPC_EXTERNC int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int batch,
                                      float* d_H, float* d_g);
+/* JCQP ADMM settings: update_solver_settings(max_iter, rho, sigma, solver_alpha, terminate, .)
+ * (convexMPC_interface.cpp:109-129 -> QpProblemSettings, JCQP/QpProblem.h:15-28). */
+typedef struct cmpc_admm_settings {
+  int    max_iter;    /* maxIterations (ros_config.yaml jcqp_max_iter: 10000)                   */
+  double rho;         /* jcqp_rho 1e-7                                                           */
+  double sigma;       /* jcqp_sigma 1e-8                                                         */
+  double alpha;       /* over-relaxation, jcqp_alpha 1.5                                         */
+  double terminate;   /* (|Ax - z|_inf + |Px + q + A'y|_inf) / 4 threshold, jcqp_terminate 0.1  */
+} cmpc_admm_settings;
+/* use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): the full QP (P = qH, q = qg from
+ * cmpc_batch_condense, A = fmat, l = 0, u = U_b) solved by JCQP's ADMM in fp64, one workgroup
+ * per instance; horizon <= 10. d_forces [batch * 12N] = jcqp.getSolution() as float;
+ * d_status 0 = residual below terminate, 1 = max_iter reached; d_iters (may be NULL). */
+CMPC_EXTERNC int cmpc_batch_admm(cmpc_batch* h, const float* d_records, const float* d_H,
+                                 const float* d_g, int batch, const cmpc_admm_settings* s,
+                                 float* d_forces, uint8_t* d_status, int32_t* d_iters);
 /* Config 5, one estimator step for every instance (SolverMPC.cpp:688-811 per instance, the
  * residual of ConvexMPCLocomotion.cpp:639-771 first when d_logs is given):
  *   f_ext  = residual(d_logs[i], d_records[i])          if d_logs  (written to d_fext6 if set)

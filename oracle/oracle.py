@@ -193,6 +193,59 @@ def est_step(state: np.ndarray, f3: float, t: float):
     return f, bool(use.value)
 
 
+# ---- use_jcqp == 1: JCQP ADMM (third_party/JCQP/QpProblem.cpp, QpProblem<double>) -----------
+def fmat_ub(rec: np.ndarray, prm):
+    """fmat (20N x 12N) and U_b (20N) as SolverMPC.cpp:646-664 builds them, in fp32."""
+    N = prm.horizon
+    mi = np.float32(1.0) / np.float32(prm.mu)
+    blk = np.array([[mi, 0, 1], [-mi, 0, 1], [0, mi, 1], [0, -mi, 1], [0, 0, 1]], np.float32)
+    A = np.zeros((20 * N, 12 * N), np.float32)
+    for b in range(4 * N):
+        A[5 * b:5 * b + 5, 3 * b:3 * b + 3] = blk
+    off = 32 + 12 * N
+    gait = np.ascontiguousarray(rec[off:off + N], np.float32).view(np.uint8)[:4 * N]
+    u = np.full(20 * N, np.float32(5e10), np.float32)
+    u[4::5] = gait.astype(np.float32) * np.float32(prm.f_max)
+    return A, u
+
+
+def jcqp_admm(P, q, A, u, max_iter=10000, rho=1e-7, sigma=1e-8, alpha=1.5, terminate=0.1):
+    """QpProblem::runFromDense restated (QpProblem.cpp:165-381, settings QpProblem.h:15-28):
+    cold start, computeConstraintInfos, the (n+m) KKT matrix factored once, then per iteration
+    stepSetup / solveLinearSystem / stepX / stepZ / stepY and every 10th iteration the residual
+    (|A x - zPrev|_inf + |P x + q + A' y|_inf) / 4. Returns (x, iterations, converged)."""
+    import scipy.linalg as sla
+    P = np.asarray(P, np.float64)
+    q = np.asarray(q, np.float64)
+    A = np.asarray(A, np.float64)
+    u = np.asarray(u, np.float64)
+    n, m = P.shape[0], A.shape[0]
+    l = np.zeros(m)
+    rh = np.where(u > 1e10, 1e-6, np.where(np.abs(u - l) < 1e-10, rho * 1e3, rho))
+    inv = 1.0 / rh
+    K = np.zeros((n + m, n + m))
+    K[:n, :n] = P + sigma * np.eye(n)
+    K[:n, n:] = A.T
+    K[n:, :n] = A
+    K[n:, n:] = -np.diag(inv)
+    lu = sla.lu_factor(K)
+    x, z, y = np.zeros(n), np.zeros(m), np.zeros(m)
+    for it in range(max_iter):
+        xp, zp = x, z
+        t = sla.lu_solve(lu, np.concatenate([sigma * xp - q, zp - inv * y]))
+        xt = t[:n]
+        zt = zp + inv * (t[n:] - y)
+        x = alpha * xt + (1 - alpha) * xp
+        zr = alpha * zt + (1 - alpha) * zp
+        z = np.clip(zr + inv * y, l, u)
+        y = y + rh * (zr - z)
+        if (it + 1) % 10 == 0:
+            res = (np.abs(P @ x + q + A.T @ y).max() + np.abs(A @ x - zp).max()) / 4
+            if res < terminate or it + 1 >= max_iter:
+                return x, it + 1, bool(res < terminate)
+    return x, max_iter, False
+
+
 # ---------------------------------------------------------------------------------------------
 # Batched input assembly (cmpc_batch_assemble): one control tick of ConvexMPCLocomotion::run's
 # MPC side per instance, restated in scalar fp32 (numpy float32: every operation rounds to fp32

@@ -269,6 +269,16 @@ extern "C" int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int ba
   return 0;
 }
 
+extern "C" int cmpc_batch_admm(cmpc_batch* h, const float* d_records, const float* d_H,
+                               const float* d_g, int batch, const cmpc_admm_settings* s,
+                               float* d_forces, uint8_t* d_status, int32_t* d_iters) {
+  if (!h || !s || batch < 0 || batch > h->max_batch) return -1;
+  hipError_t e = cmpc::launch_admm(d_records, d_H, d_g, batch, h->kp, *s, d_forces, d_status,
+                                   d_iters, h->stream);
+  if (e != hipSuccess) return fail("launch_admm", e);
+  return 0;
+}
+
 static int ensure_staging(cmpc_batch* h) {
   if (h->d_rec) return 0;
   const size_t words = (size_t)CMPC_REC_WORDS(CMPC_MAX_HORIZON) * h->max_batch;

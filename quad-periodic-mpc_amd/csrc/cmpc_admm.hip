@@ -1,0 +1,215 @@
+// cmpc_admm.hip — batched JCQP ADMM, the use_jcqp == 1 branch of solve_mpc (SURVEY.md §8(f)
+// rank 4; SolverMPC.cpp:818-838 and :1057-1062, third_party/JCQP/QpProblem.cpp:165-381).
+//
+// One workgroup (256 lanes, 4 wavefronts) per instance, fp64 like QpProblem<double>:
+//   P = qH, q = qg (the full fp32 condensation of cmpc_batch_condense, cast to double),
+//   A = fmat (20N x 12N, 5x3 friction-pyramid blocks), l = 0, u = U_b (5e10 / gait*f_max).
+// computeConstraintInfos (QpProblem.cpp:255-272) picks rho per row: u > infty -> rhoInfty,
+// |u - l| < eqlTol (swing fz rows) -> rho*rhoEqualityScale, else rho.
+// The KKT system [P + sigma I, A'; A, -diag(1/rho)] is solved through its Schur complement
+// M = P + sigma I + A' diag(rho) A (block-diagonal A'rhoA: 3x3 per foot-step), inverted once in
+// LDS by Gauss-Jordan (SPD, no pivoting); per iteration xt = M^-1 (sigma xp - q + A'(rho zp - y))
+// and zt = A xt, which is what solveLinearSystem's "step!" line produces. stepX / stepZ / stepY
+// and the every-10-iterations residual (p + d) / 4 against _zPrev follow QpProblem.cpp:306-381.
+// Horizon N <= 10 (M is 12N x 12N doubles resident in LDS: 115 KB at N = 10).
+#include "cmpc_kernels.h"
+
+namespace cmpc {
+namespace {
+
+constexpr int kAdmmThreads = 256;
+constexpr int kAdmmMaxN = 10;
+constexpr int kNV = 12 * kAdmmMaxN;   // 120 variables
+constexpr int kNC = 20 * kAdmmMaxN;   // 200 constraints
+
+struct AdmmParams {
+  double rho, sigma, alpha, terminate;
+  int max_iter;
+  int N;
+  int rec_words;
+  float mu_inv;
+  float f_max;
+};
+
+// fmat row k (0..4) of a 5x3 block, column a (SolverMPC.cpp:657-664)
+__device__ __forceinline__ double fcoef(int k, int a, double mi) {
+  // [[mi,0,1],[-mi,0,1],[0,mi,1],[0,-mi,1],[0,0,1]]
+  if (a == 2) return 1.0;
+  if (k == 4) return 0.0;
+  if (a == 0) return k == 0 ? mi : (k == 1 ? -mi : 0.0);
+  return k == 2 ? mi : (k == 3 ? -mi : 0.0);
+}
+
+__device__ __forceinline__ double block_max(double v, double* red) {
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int s = kAdmmThreads / 2; s > 0; s >>= 1) {
+    if (t < s) red[t] = fmax(red[t], red[t + s]);
+    __syncthreads();
+  }
+  double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(kAdmmThreads)
+cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
+                 const float* __restrict__ gg, AdmmParams ap, float* __restrict__ forces,
+                 uint8_t* __restrict__ status, int32_t* __restrict__ iters) {
+  __shared__ double M[kNV * kNV];
+  __shared__ double sx[2][kNV], sz[2][kNV > kNC ? kNV : kNC];
+  __shared__ double sy[kNC], sq[kNV], srhs[kNV], sxt[kNV], srho[kNC], su[kNC];
+  __shared__ double red[kAdmmThreads];
+  const int t = threadIdx.x;
+  const int inst = blockIdx.x;
+  const int n = 12 * ap.N, m = 20 * ap.N;
+  const float* H = gH + (size_t)inst * n * n;
+  const float* rec = recs + (size_t)inst * ap.rec_words;
+  const uint8_t* gait = reinterpret_cast<const uint8_t*>(rec + CMPC_REC_HDR + 12 * ap.N);
+  const double mi = (double)ap.mu_inv;
+
+  // ---- setup: P + sigma I, q, u, rho; cold start (QpProblem.cpp:9-20) ----
+  for (int e = t; e < n * n; e += kAdmmThreads) {
+    const int i = e / n, j = e - i * n;
+    M[e] = (double)H[e] + (i == j ? ap.sigma : 0.0);
+  }
+  for (int i = t; i < n; i += kAdmmThreads) {
+    sq[i] = (double)gg[(size_t)inst * n + i];
+    sx[0][i] = 0.0;
+    sx[1][i] = 0.0;
+  }
+  for (int r = t; r < m; r += kAdmmThreads) {
+    const int b = r / 5, k = r - 5 * b;
+    // U_b (SolverMPC.cpp:646-652): 5e10 for the four pyramid rows, gait * f_max for fz
+    const double u = k < 4 ? (double)5e10f : (double)((float)gait[b] * ap.f_max);
+    double rho;
+    if (u > 1e10) rho = 1e-6;                        // INFINITE: rhoInfty
+    else if (fabs(u) < 1e-10) rho = ap.rho * 1e3;   // EQUALITY: rho * rhoEqualityScale
+    else rho = ap.rho;
+    su[r] = u;
+    srho[r] = rho;
+    sy[r] = 0.0;
+    sz[0][r] = 0.0;
+    sz[1][r] = 0.0;
+  }
+  __syncthreads();
+  // A' diag(rho) A: block-diagonal, 3x3 per foot-step b (variables 3b..3b+2, rows 5b..5b+4)
+  for (int e = t; e < 9 * (n / 3); e += kAdmmThreads) {
+    const int b = e / 9, a0 = (e - 9 * b) / 3, a1 = e - 9 * b - 3 * a0;
+    double s = 0.0;
+    for (int k = 0; k < 5; ++k) s += srho[5 * b + k] * fcoef(k, a0, mi) * fcoef(k, a1, mi);
+    M[(3 * b + a0) * n + 3 * b + a1] += s;
+  }
+  __syncthreads();
+
+  // ---- Gauss-Jordan inverse in place (SPD: no pivoting) ----
+  for (int k = 0; k < n; ++k) {
+    const double piv = 1.0 / M[k * n + k];
+    for (int j = t; j < n; j += kAdmmThreads)
+      if (j != k) M[k * n + j] *= piv;
+    __syncthreads();
+    for (int e = t; e < n * n; e += kAdmmThreads) {
+      const int i = e / n, j = e - i * n;
+      if (i != k && j != k) M[e] -= M[i * n + k] * M[k * n + j];
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += kAdmmThreads)
+      if (i != k) M[i * n + k] *= -piv;
+    if (t == 0) M[k * n + k] = piv;
+    __syncthreads();
+  }
+
+  // ---- ADMM iterations (runFromDense, QpProblem.cpp:165-225) ----
+  const double al = ap.alpha, sg = ap.sigma;
+  int cur = 0;                 // sx[cur] / sz[cur] hold _x / _z
+  int it_done = ap.max_iter;
+  uint8_t st = 1;
+  for (int it = 0; it < ap.max_iter; ++it) {
+    const int prv = cur;       // stepSetup: swap, the old _x becomes _xPrev
+    cur ^= 1;
+    const double* xp = sx[prv];
+    const double* zp = sz[prv];
+    // rhs = sigma xp - q + A'(rho zp - y)
+    for (int i = t; i < n; i += kAdmmThreads) {
+      const int b = i / 3, a = i - 3 * b;
+      double s = sg * xp[i] - sq[i];
+      for (int k = 0; k < 5; ++k) {
+        const int r = 5 * b + k;
+        s += fcoef(k, a, mi) * (srho[r] * zp[r] - sy[r]);
+      }
+      srhs[i] = s;
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += kAdmmThreads) {
+      double s = 0.0;
+      for (int j = 0; j < n; ++j) s += M[j * n + i] * srhs[j];   // M^-1 symmetric: column read
+      sxt[i] = s;
+      sx[cur][i] = al * s + (1.0 - al) * xp[i];                 // stepX
+    }
+    __syncthreads();
+    for (int r = t; r < m; r += kAdmmThreads) {                 // stepZ, stepY
+      const int b = r / 5, k = r - 5 * b;
+      double zt = 0.0;
+      for (int a = 0; a < 3; ++a) zt += fcoef(k, a, mi) * sxt[3 * b + a];
+      const double zr = al * zt + (1.0 - al) * zp[r];
+      double z = zr + sy[r] / srho[r];
+      if (z < 0.0) z = 0.0;
+      if (z > su[r]) z = su[r];
+      sz[cur][r] = z;
+      sy[r] += srho[r] * (zr - z);
+    }
+    __syncthreads();
+    if ((it + 1) % 10 == 0) {
+      // p = |A x - zPrev|_inf, d = |P x + q + A' y|_inf  (calcAndDisplayResidual, dense branch)
+      const double* x = sx[cur];
+      double pm = 0.0, dm = 0.0;
+      for (int r = t; r < m; r += kAdmmThreads) {
+        const int b = r / 5, k = r - 5 * b;
+        double ax = 0.0;
+        for (int a = 0; a < 3; ++a) ax += fcoef(k, a, mi) * x[3 * b + a];
+        pm = fmax(pm, fabs(ax - zp[r]));
+      }
+      for (int i = t; i < n; i += kAdmmThreads) {
+        const float* Hi = H + (size_t)i * n;
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += (double)Hi[j] * x[j];
+        s += sq[i];
+        const int b = i / 3, a = i - 3 * b;
+        for (int k = 0; k < 5; ++k) s += fcoef(k, a, mi) * sy[5 * b + k];
+        dm = fmax(dm, fabs(s));
+      }
+      const double p = block_max(pm, red);
+      const double d = block_max(dm, red);
+      const double res = (d + p) / 4;
+      if (res < ap.terminate || it + 1 >= ap.max_iter) {
+        it_done = it + 1;
+        st = res < ap.terminate ? 0 : 1;
+        break;
+      }
+    }
+  }
+  // q_soln[i] = jcqp.getSolution()[i] (SolverMPC.cpp:1057-1062)
+  for (int i = t; i < n; i += kAdmmThreads) forces[(size_t)inst * n + i] = (float)sx[cur][i];
+  if (t == 0) {
+    status[inst] = st;
+    if (iters) iters[inst] = it_done;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_admm(const float* d_recs, const float* d_H, const float* d_g, int batch,
+                       const KParams& P, const cmpc_admm_settings& s, float* d_forces,
+                       uint8_t* d_status, int32_t* d_iters, hipStream_t stream) {
+  if (P.N < 1 || P.N > kAdmmMaxN || s.max_iter < 1 || !(s.rho > 0) || !(s.alpha > 0))
+    return hipErrorInvalidValue;
+  if (batch == 0) return hipSuccess;
+  AdmmParams ap{s.rho, s.sigma, s.alpha, s.terminate, s.max_iter, P.N, P.rec_words, P.mu_inv,
+                P.f_max};
+  hipLaunchKernelGGL(cmpc_admm_kernel, dim3(batch), dim3(kAdmmThreads), 0, stream, d_recs, d_H,
+                     d_g, ap, d_forces, d_status, d_iters);
+  return hipGetLastError();
+}
+
+}  // namespace cmpc

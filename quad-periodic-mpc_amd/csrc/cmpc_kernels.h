@@ -90,4 +90,9 @@ hipError_t launch_rollout(float* d_loco, const float* d_recs, const float* d_for
 hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
                            float* scratch, int grid, hipStream_t stream);
 
+// use_jcqp == 1: batched JCQP ADMM over the full condensed QP (cmpc_admm.hip)
+hipError_t launch_admm(const float* d_recs, const float* d_H, const float* d_g, int batch,
+                       const KParams& P, const cmpc_admm_settings& s, float* d_forces,
+                       uint8_t* d_status, int32_t* d_iters, hipStream_t stream);
+
 }  // namespace cmpc

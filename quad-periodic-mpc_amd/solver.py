@@ -45,6 +45,17 @@ class CmpcError(RuntimeError):
     pass
 
 
+class AdmmSettings(ctypes.Structure):
+    """cmpc_admm_settings (include/cmpc_solver.h); defaults = ros_config.yaml:73-77."""
+    _fields_ = [("max_iter", ctypes.c_int), ("rho", ctypes.c_double), ("sigma", ctypes.c_double),
+                ("alpha", ctypes.c_double), ("terminate", ctypes.c_double)]
+
+
+def admm_settings(max_iter: int = 10000, rho: float = 1e-7, sigma: float = 1e-8,
+                  alpha: float = 1.5, terminate: float = 0.1) -> AdmmSettings:
+    return AdmmSettings(int(max_iter), float(rho), float(sigma), float(alpha), float(terminate))
+
+
 def load_library(path: str = LIB_PATH):
     """Load libcmpc_hip.so (fails loudly if it has not been built)."""
     global _lib
@@ -76,6 +87,9 @@ def load_library(path: str = LIB_PATH):
     lib.cmpc_batch_solve_host.argtypes = [ctypes.c_void_p, _fp, ctypes.c_int, _fp, _u8p, _ip]
     lib.cmpc_batch_condense.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p]
+    lib.cmpc_batch_admm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(AdmmSettings),
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.cmpc_batch_stream.argtypes = [ctypes.c_void_p]
     lib.cmpc_batch_stream.restype = ctypes.c_void_p
     lib.cmpc_last_error.restype = ctypes.c_char_p
@@ -235,6 +249,17 @@ class BatchSolver:
             batch = records.shape[0]
         _check(self.lib.cmpc_batch_condense(self._h, _ptr(records), int(batch), _ptr(H), _ptr(g)),
                "cmpc_batch_condense")
+
+    def admm(self, records, H, g, forces, status, iters=None, settings: AdmmSettings | None = None,
+             batch: int | None = None) -> None:
+        """use_jcqp == 1 on device (``cmpc_batch_admm``): JCQP's ADMM over the full QP whose
+        ``H`` / ``g`` came from :meth:`condense`."""
+        if batch is None:
+            batch = records.shape[0]
+        s = settings if settings is not None else admm_settings()
+        _check(self.lib.cmpc_batch_admm(self._h, _ptr(records), _ptr(H), _ptr(g), int(batch),
+                                        ctypes.byref(s), _ptr(forces), _ptr(status), _ptr(iters)),
+               "cmpc_batch_admm")
 
     def estimate(self, est_state, records, *, logs=None, fext3=None, times=None,
                  sim_time: float = 0.0, fext6=None, batch: int | None = None) -> None:
