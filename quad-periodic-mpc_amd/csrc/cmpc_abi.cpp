@@ -425,6 +425,31 @@ void estimator_step(SingleState& s) {
   s.f_est_static[3] = 0.97f * s.f_est_static[3] + 0.03f * f_ext[3];
 }
 
+// One instance through condense + ADMM on the handle's stream (host record in, host forces out).
+int admm_host(cmpc_batch* h, const float* rec, int N, const cmpc_admm_settings& as, float* forces,
+              uint8_t* st) {
+  if (int r = ensure_staging(h)) return r;
+  const size_t n = 12 * (size_t)N;
+  float *dH = nullptr, *dg = nullptr;
+  hipError_t e;
+  if ((e = hipMalloc(&dH, (n * n + n) * sizeof(float))) != hipSuccess) return fail("hipMalloc", e);
+  dg = dH + n * n;
+  int rc = 0;
+  if ((e = hipMemcpyAsync(h->d_rec, rec, CMPC_REC_WORDS(N) * sizeof(float), hipMemcpyHostToDevice,
+                          h->stream)) != hipSuccess)
+    rc = fail("H2D", e);
+  if (!rc) rc = cmpc_batch_condense(h, h->d_rec, 1, dH, dg);
+  if (!rc) rc = cmpc_batch_admm(h, h->d_rec, dH, dg, 1, &as, h->d_forces, h->d_status, nullptr);
+  if (!rc && (e = hipMemcpyAsync(forces, h->d_forces, n * sizeof(float), hipMemcpyDeviceToHost,
+                                 h->stream)) != hipSuccess)
+    rc = fail("D2H", e);
+  if (!rc && (e = hipMemcpyAsync(st, h->d_status, 1, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+    rc = fail("D2H", e);
+  if (!rc && (e = hipStreamSynchronize(h->stream)) != hipSuccess) rc = fail("sync", e);
+  (void)hipFree(dH);
+  return rc;
+}
+
 void solve_single(SingleState& s) {
   const int N = s.cfg.horizon;
   if (N < 1 || N > CMPC_MAX_HORIZON) {
@@ -466,6 +491,19 @@ void solve_single(SingleState& s) {
 
   std::vector<float> forces(12 * N);
   uint8_t st = 0;
+  if (s.use_jcqp == 1 && N <= 10) {
+    // use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): ADMM over the full QP, no elimination;
+    // the reference keeps jcqp's solution whatever the residual, so no failure message
+    cmpc_admm_settings as{s.max_iterations, s.rho, s.sigma, s.solver_alpha, s.terminate};
+    if (admm_host(s.h, rec.data(), N, as, forces.data(), &st) != 0) {
+      std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
+      return;
+    }
+    s.q_soln.assign(12 * N, 0.0);
+    for (int i = 0; i < 12 * N; i++) s.q_soln[i] = forces[i];
+    s.has_solved = 1;
+    return;
+  }
   if (cmpc_batch_solve_host(s.h, rec.data(), 1, forces.data(), &st, nullptr) != 0) {
     std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
     return;
@@ -499,7 +537,8 @@ extern "C" void update_solver_settings(int max_iter, double rho, double sigma, d
   g.solver_alpha = solver_alpha;
   g.terminate = terminate;
   g.use_jcqp = use_jcqp > 1.5 ? 2 : (use_jcqp > 0.5 ? 1 : 0);
-  if (g.use_jcqp != 0) std::fprintf(stderr, "[cmpc] use_jcqp=%d: JCQP is not built; dense active-set QP used\n", g.use_jcqp);
+  // use_jcqp == 1 runs the ADMM kernel (N <= 10); the reduced ADMM (2) is not built
+  if (g.use_jcqp == 2) std::fprintf(stderr, "[cmpc] use_jcqp=2: reduced JCQP not built; dense active-set QP used\n");
 }
 
 extern "C" void update_problem_data_floats(float* p, float* v, float* q, float* w, float* r, float roll,

@@ -141,11 +141,27 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
       srhs[i] = s;
     }
     __syncthreads();
-    for (int i = t; i < n; i += kAdmmThreads) {
-      double s = 0.0;
-      for (int j = 0; j < n; ++j) s += M[j * n + i] * srhs[j];   // M^-1 symmetric: column read
-      sxt[i] = s;
-      sx[cur][i] = al * s + (1.0 - al) * xp[i];                 // stepX
+    // xt = M^-1 rhs: two adjacent lanes per row, each half of the columns with four
+    // independent accumulators (the LDS reads pipeline instead of one serial FMA chain), then a
+    // lane-pair shuffle; M^-1 is symmetric, so lanes of a row read down a column
+    if (t < 2 * n) {
+      const int i = t >> 1, h = t & 1, half = n >> 1;   // n = 12N: half = 6N, even
+      const int j0 = h * half, j1 = j0 + half;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      int j = j0;
+      for (; j + 4 <= j1; j += 4) {
+        a0 += M[(j + 0) * n + i] * srhs[j + 0];
+        a1 += M[(j + 1) * n + i] * srhs[j + 1];
+        a2 += M[(j + 2) * n + i] * srhs[j + 2];
+        a3 += M[(j + 3) * n + i] * srhs[j + 3];
+      }
+      for (; j < j1; ++j) a0 += M[j * n + i] * srhs[j];
+      double s = (a0 + a1) + (a2 + a3);
+      s += __shfl_xor(s, 1);
+      if (h == 0) {
+        sxt[i] = s;
+        sx[cur][i] = al * s + (1.0 - al) * xp[i];               // stepX
+      }
     }
     __syncthreads();
     for (int r = t; r < m; r += kAdmmThreads) {                 // stepZ, stepY
@@ -172,9 +188,14 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
       }
       for (int i = t; i < n; i += kAdmmThreads) {
         const float* Hi = H + (size_t)i * n;
-        double s = 0.0;
-        for (int j = 0; j < n; ++j) s += (double)Hi[j] * x[j];
-        s += sq[i];
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        for (int j = 0; j < n; j += 4) {
+          a0 += (double)Hi[j + 0] * x[j + 0];
+          a1 += (double)Hi[j + 1] * x[j + 1];
+          a2 += (double)Hi[j + 2] * x[j + 2];
+          a3 += (double)Hi[j + 3] * x[j + 3];
+        }
+        double s = (a0 + a1) + (a2 + a3) + sq[i];
         const int b = i / 3, a = i - 3 * b;
         for (int k = 0; k < 5; ++k) s += fcoef(k, a, mi) * sy[5 * b + k];
         dm = fmax(dm, fabs(s));

@@ -72,6 +72,23 @@ def test_admm_kernel_matches_oracle(cm, orc, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 5])
+def test_admm_short_horizons_match_oracle(cm, orc, N):
+    solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+    solver_mod.load_library()
+    prm = cm.make_params(N)
+    recs = cm.make_instances(16, N, seed=99 + N)
+    H, gv, f, status, iters = _run(cm, solver_mod, recs, prm, TIGHT)
+    for i in range(recs.shape[0]):
+        A, u = orc.fmat_ub(recs[i], prm)
+        x, it, ok = orc.jcqp_admm(H[i], gv[i], A, u, **TIGHT)
+        if iters[i] == it:
+            assert rel_force_err(f[i:i + 1], x[None])[0] <= 1e-6, (i, it)
+        else:
+            assert rel_force_err(f[i:i + 1], x[None])[0] <= 1e-3, (i, it, iters[i])
+
+
+@pytest.mark.gpu
 def test_admm_tight_matches_qpoases(cm):
     solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
     solver_mod.load_library()
@@ -93,3 +110,30 @@ def test_admm_rejects_long_horizon(cm):
     with pytest.raises(solver_mod.CmpcError):
         _run(cm, solver_mod, recs, prm, TIGHT)
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_reference_call_protocol_use_jcqp(cm):
+    """update_solver_settings(..., use_jcqp = 1) routes the batch-1 ABI solve through the ADMM
+    kernel (SolverMPC.cpp:818-838); tight settings reach the qpOASES optimum."""
+    solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+    solver_mod.load_library()
+    N = 10
+    prm = cm.make_params(N)
+    g = load_golden("n10_mixed")
+    try:
+        for i in range(3):
+            rec = g["records"][i]
+            solver_mod.setup_problem(0.026, N, 0.4, 120)
+            solver_mod.update_x_drag(float(rec[28]))
+            solver_mod.update_solver_settings(TIGHT["max_iter"], TIGHT["rho"], TIGHT["sigma"],
+                                              TIGHT["alpha"], TIGHT["terminate"], 1.0)
+            gait = cm.unpack_gait(rec[None], N)[0].astype(np.int32)
+            solver_mod.update_problem_data_floats(rec[0:3], rec[3:6], rec[6:10], rec[10:13],
+                                                  rec[13:25], rec[25], rec[26], rec[27],
+                                                  np.array(prm.weights), rec[32:32 + 12 * N],
+                                                  prm.alpha, gait)
+            sol = np.array([solver_mod.get_solution(j) for j in range(12 * N)])
+            assert rel_force_err(sol[None], g["q_ref"][i][None]).max() <= 5e-5
+    finally:
+        solver_mod.update_solver_settings(100, 1e-7, 1e-8, 1.5, 1e-5, 0)
