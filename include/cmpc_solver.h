@@ -202,11 +202,15 @@ typedef struct cmpc_admm_settings {
   double sigma;       /* jcqp_sigma 1e-8                                                         */
   double alpha;       /* over-relaxation, jcqp_alpha 1.5                                         */
   double terminate;   /* (|Ax - z|_inf + |Px + q + A'y|_inf) / 4 threshold, jcqp_terminate 0.1  */
+  int    reduced;     /* 0: use_jcqp == 1 (full QP); 1: use_jcqp == 2 (swing legs eliminated)    */
 } cmpc_admm_settings;
 /* use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): the full QP (P = qH, q = qg from
  * cmpc_batch_condense, A = fmat, l = 0, u = U_b) solved by JCQP's ADMM in fp64, one workgroup
- * per instance; horizon <= 10. d_forces [batch * 12N] = jcqp.getSolution() as float;
- * d_status 0 = residual below terminate, 1 = max_iter reached; d_iters (may be NULL). */
+ * per instance; horizon <= 10. With s->reduced (use_jcqp == 2, SolverMPC.cpp:984-1053) the
+ * swing legs are eliminated first and any horizon is accepted while 3 x (stance foot-steps)
+ * <= 120 (else status CMPC_BAD_INPUT, zeros). d_forces [batch * 12N] = the solution as float
+ * (0 for eliminated variables); d_status 0 = residual below terminate, 1 = max_iter reached;
+ * d_iters (may be NULL). */
 CMPC_EXTERNC int cmpc_batch_admm(cmpc_batch* h, const float* d_records, const float* d_H,
                                  const float* d_g, int batch, const cmpc_admm_settings* s,
                                  float* d_forces, uint8_t* d_status, int32_t* d_iters);

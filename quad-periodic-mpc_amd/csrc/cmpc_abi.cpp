@@ -491,10 +491,12 @@ void solve_single(SingleState& s) {
 
   std::vector<float> forces(12 * N);
   uint8_t st = 0;
-  if (s.use_jcqp == 1 && N <= 10) {
-    // use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): ADMM over the full QP, no elimination;
-    // the reference keeps jcqp's solution whatever the residual, so no failure message
-    cmpc_admm_settings as{s.max_iterations, s.rho, s.sigma, s.solver_alpha, s.terminate};
+  if ((s.use_jcqp == 1 && N <= 10) || s.use_jcqp == 2) {
+    // use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): ADMM over the full QP; use_jcqp == 2
+    // (:984-1053): over the reduced one. The reference keeps JCQP's solution whatever the
+    // residual, so no failure message
+    cmpc_admm_settings as{s.max_iterations, s.rho, s.sigma, s.solver_alpha, s.terminate,
+                          s.use_jcqp == 2 ? 1 : 0};
     if (admm_host(s.h, rec.data(), N, as, forces.data(), &st) != 0) {
       std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
       return;
@@ -537,8 +539,7 @@ extern "C" void update_solver_settings(int max_iter, double rho, double sigma, d
   g.solver_alpha = solver_alpha;
   g.terminate = terminate;
   g.use_jcqp = use_jcqp > 1.5 ? 2 : (use_jcqp > 0.5 ? 1 : 0);
-  // use_jcqp == 1 runs the ADMM kernel (N <= 10); the reduced ADMM (2) is not built
-  if (g.use_jcqp == 2) std::fprintf(stderr, "[cmpc] use_jcqp=2: reduced JCQP not built; dense active-set QP used\n");
+  // use_jcqp == 1 / 2 run the ADMM kernel (full QP for N <= 10 / reduced QP)
 }
 
 extern "C" void update_problem_data_floats(float* p, float* v, float* q, float* w, float* r, float roll,

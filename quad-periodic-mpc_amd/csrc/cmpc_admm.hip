@@ -11,7 +11,8 @@
 // LDS by Gauss-Jordan (SPD, no pivoting); per iteration xt = M^-1 (sigma xp - q + A'(rho zp - y))
 // and zt = A xt, which is what solveLinearSystem's "step!" line produces. stepX / stepZ / stepY
 // and the every-10-iterations residual (p + d) / 4 against _zPrev follow QpProblem.cpp:306-381.
-// Horizon N <= 10 (M is 12N x 12N doubles resident in LDS: 115 KB at N = 10).
+// M (n x n doubles) is resident in LDS, n <= 120: the full QP up to N = 10; the reduced one
+// (use_jcqp == 2) while 3 x (stance foot-steps) <= 120, e.g. trot up to N = 20.
 #include "cmpc_kernels.h"
 
 namespace cmpc {
@@ -29,6 +30,7 @@ struct AdmmParams {
   int rec_words;
   float mu_inv;
   float f_max;
+  int reduced;   // use_jcqp == 2: swing legs eliminated first (SolverMPC.cpp:859-950, 984-1053)
 };
 
 // fmat row k (0..4) of a 5x3 block, column a (SolverMPC.cpp:657-664)
@@ -61,28 +63,53 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
   __shared__ double sx[2][kNV], sz[2][kNV > kNC ? kNV : kNC];
   __shared__ double sy[kNC], sq[kNV], srhs[kNV], sxt[kNV], srho[kNC], su[kNC];
   __shared__ double red[kAdmmThreads];
+  __shared__ int smap[4 * CMPC_MAX_HORIZON];   // compact foot-step -> foot-step (variables 3b..)
+  __shared__ int sinv[4 * CMPC_MAX_HORIZON];   // foot-step -> compact, -1 if eliminated
+  __shared__ int snb;
   const int t = threadIdx.x;
   const int inst = blockIdx.x;
-  const int n = 12 * ap.N, m = 20 * ap.N;
-  const float* H = gH + (size_t)inst * n * n;
+  const int nf = 12 * ap.N;                    // full variable count = qH stride
+  const float* H = gH + (size_t)inst * nf * nf;
   const float* rec = recs + (size_t)inst * ap.rec_words;
   const uint8_t* gait = reinterpret_cast<const uint8_t*>(rec + CMPC_REC_HDR + 12 * ap.N);
   const double mi = (double)ap.mu_inv;
+  // Elimination (reduced mode): a foot-step whose fz row has lb = ub = 0 (gait 0) loses its three
+  // variables and five rows; the kept ones stay in order (SolverMPC.cpp:859-950)
+  if (t == 0) {
+    int c = 0;
+    for (int b = 0; b < 4 * ap.N; ++b) {
+      const bool keep = !ap.reduced || gait[b] != 0;
+      sinv[b] = keep ? c : -1;
+      if (keep) smap[c++] = b;
+    }
+    snb = c;
+  }
+  __syncthreads();
+  const int nb = snb, n = 3 * nb, m = 5 * nb;
+  if (n > kNV) {               // reduced problem still too large for the LDS-resident inverse
+    for (int v = t; v < nf; v += kAdmmThreads) forces[(size_t)inst * nf + v] = 0.f;
+    if (t == 0) {
+      status[inst] = CMPC_BAD_INPUT;
+      if (iters) iters[inst] = 0;
+    }
+    return;
+  }
 
   // ---- setup: P + sigma I, q, u, rho; cold start (QpProblem.cpp:9-20) ----
   for (int e = t; e < n * n; e += kAdmmThreads) {
     const int i = e / n, j = e - i * n;
-    M[e] = (double)H[e] + (i == j ? ap.sigma : 0.0);
+    const int fi = 3 * smap[i / 3] + i % 3, fj = 3 * smap[j / 3] + j % 3;
+    M[e] = (double)H[(size_t)fi * nf + fj] + (i == j ? ap.sigma : 0.0);
   }
   for (int i = t; i < n; i += kAdmmThreads) {
-    sq[i] = (double)gg[(size_t)inst * n + i];
+    sq[i] = (double)gg[(size_t)inst * nf + 3 * smap[i / 3] + i % 3];
     sx[0][i] = 0.0;
     sx[1][i] = 0.0;
   }
   for (int r = t; r < m; r += kAdmmThreads) {
     const int b = r / 5, k = r - 5 * b;
     // U_b (SolverMPC.cpp:646-652): 5e10 for the four pyramid rows, gait * f_max for fz
-    const double u = k < 4 ? (double)5e10f : (double)((float)gait[b] * ap.f_max);
+    const double u = k < 4 ? (double)5e10f : (double)((float)gait[smap[b]] * ap.f_max);
     double rho;
     if (u > 1e10) rho = 1e-6;                        // INFINITE: rhoInfty
     else if (fabs(u) < 1e-10) rho = ap.rho * 1e3;   // EQUALITY: rho * rhoEqualityScale
@@ -145,8 +172,8 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
     // independent accumulators (the LDS reads pipeline instead of one serial FMA chain), then a
     // lane-pair shuffle; M^-1 is symmetric, so lanes of a row read down a column
     if (t < 2 * n) {
-      const int i = t >> 1, h = t & 1, half = n >> 1;   // n = 12N: half = 6N, even
-      const int j0 = h * half, j1 = j0 + half;
+      const int i = t >> 1, h = t & 1, half = n >> 1;   // n = 3 x kept foot-steps: may be odd
+      const int j0 = h ? half : 0, j1 = h ? n : half;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       int j = j0;
       for (; j + 4 <= j1; j += 4) {
@@ -187,15 +214,15 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
         pm = fmax(pm, fabs(ax - zp[r]));
       }
       for (int i = t; i < n; i += kAdmmThreads) {
-        const float* Hi = H + (size_t)i * n;
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        for (int j = 0; j < n; j += 4) {
-          a0 += (double)Hi[j + 0] * x[j + 0];
-          a1 += (double)Hi[j + 1] * x[j + 1];
-          a2 += (double)Hi[j + 2] * x[j + 2];
-          a3 += (double)Hi[j + 3] * x[j + 3];
+        const float* Hi = H + (size_t)(3 * smap[i / 3] + i % 3) * nf;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+        for (int c = 0; c < nb; ++c) {     // the kept columns, one foot-step (3 wide) at a time
+          const float* h = Hi + 3 * smap[c];
+          a0 += (double)h[0] * x[3 * c + 0];
+          a1 += (double)h[1] * x[3 * c + 1];
+          a2 += (double)h[2] * x[3 * c + 2];
         }
-        double s = (a0 + a1) + (a2 + a3) + sq[i];
+        double s = (a0 + a1) + a2 + sq[i];
         const int b = i / 3, a = i - 3 * b;
         for (int k = 0; k < 5; ++k) s += fcoef(k, a, mi) * sy[5 * b + k];
         dm = fmax(dm, fabs(s));
@@ -211,7 +238,11 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
     }
   }
   // q_soln[i] = jcqp.getSolution()[i] (SolverMPC.cpp:1057-1062)
-  for (int i = t; i < n; i += kAdmmThreads) forces[(size_t)inst * n + i] = (float)sx[cur][i];
+  // q_soln: eliminated variables 0 (reduced), else reducedProblem / jcqp.getSolution()
+  for (int v = t; v < nf; v += kAdmmThreads) {
+    const int c = sinv[v / 3];
+    forces[(size_t)inst * nf + v] = c < 0 ? 0.f : (float)sx[cur][3 * c + v % 3];
+  }
   if (t == 0) {
     status[inst] = st;
     if (iters) iters[inst] = it_done;
@@ -223,11 +254,12 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
 hipError_t launch_admm(const float* d_recs, const float* d_H, const float* d_g, int batch,
                        const KParams& P, const cmpc_admm_settings& s, float* d_forces,
                        uint8_t* d_status, int32_t* d_iters, hipStream_t stream) {
-  if (P.N < 1 || P.N > kAdmmMaxN || s.max_iter < 1 || !(s.rho > 0) || !(s.alpha > 0))
+  if (P.N < 1 || P.N > (s.reduced ? CMPC_MAX_HORIZON : kAdmmMaxN) || s.max_iter < 1 ||
+      !(s.rho > 0) || !(s.alpha > 0))
     return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
   AdmmParams ap{s.rho, s.sigma, s.alpha, s.terminate, s.max_iter, P.N, P.rec_words, P.mu_inv,
-                P.f_max};
+                P.f_max, s.reduced ? 1 : 0};
   hipLaunchKernelGGL(cmpc_admm_kernel, dim3(batch), dim3(kAdmmThreads), 0, stream, d_recs, d_H,
                      d_g, ap, d_forces, d_status, d_iters);
   return hipGetLastError();

@@ -48,12 +48,14 @@ class CmpcError(RuntimeError):
 class AdmmSettings(ctypes.Structure):
     """cmpc_admm_settings (include/cmpc_solver.h); defaults = ros_config.yaml:73-77."""
     _fields_ = [("max_iter", ctypes.c_int), ("rho", ctypes.c_double), ("sigma", ctypes.c_double),
-                ("alpha", ctypes.c_double), ("terminate", ctypes.c_double)]
+                ("alpha", ctypes.c_double), ("terminate", ctypes.c_double),
+                ("reduced", ctypes.c_int)]
 
 
 def admm_settings(max_iter: int = 10000, rho: float = 1e-7, sigma: float = 1e-8,
-                  alpha: float = 1.5, terminate: float = 0.1) -> AdmmSettings:
-    return AdmmSettings(int(max_iter), float(rho), float(sigma), float(alpha), float(terminate))
+                  alpha: float = 1.5, terminate: float = 0.1, reduced: bool = False) -> AdmmSettings:
+    return AdmmSettings(int(max_iter), float(rho), float(sigma), float(alpha), float(terminate),
+                        int(bool(reduced)))
 
 
 def load_library(path: str = LIB_PATH):

@@ -137,3 +137,53 @@ def test_reference_call_protocol_use_jcqp(cm):
             assert rel_force_err(sol[None], g["q_ref"][i][None]).max() <= 5e-5
     finally:
         solver_mod.update_solver_settings(100, 1e-7, 1e-8, 1.5, 1e-5, 0)
+
+
+def _kept(rec, prm):
+    """Variable indices kept by the swing elimination (SolverMPC.cpp:859-950): stance foot-steps."""
+    gait = np.asarray(importlib.import_module("quad-periodic-mpc_amd").unpack_gait(
+        rec[None], prm.horizon)[0]).reshape(-1)
+    return np.concatenate([np.arange(3 * b, 3 * b + 3) for b in range(gait.size) if gait[b]]
+                          or [np.zeros(0, int)]).astype(int)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["n10_mixed", "n20_trot"])
+def test_admm_reduced_matches_oracle(cm, orc, name):
+    """use_jcqp == 2: elimination, then ADMM on the reduced QP (SolverMPC.cpp:984-1053)."""
+    solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+    solver_mod.load_library()
+    g = load_golden(name)
+    prm = golden_params(cm, g)
+    recs = g["records"][:24]
+    settings = dict(max_iter=10000, rho=1e-7, sigma=1e-8, alpha=1.5, terminate=0.1)
+    H, gv, f, status, iters = _run(cm, solver_mod, recs, prm, dict(settings, reduced=True))
+    same = 0
+    for i in range(recs.shape[0]):
+        A, u = orc.fmat_ub(recs[i], prm)
+        kv = _kept(recs[i], prm)
+        kr = np.concatenate([np.arange(5 * (v // 3), 5 * (v // 3) + 5) for v in kv[::3]]
+                            or [np.zeros(0, int)]).astype(int)
+        x, it, ok = orc.jcqp_admm(H[i][np.ix_(kv, kv)], gv[i][kv], A[np.ix_(kr, kv)], u[kr],
+                                  **settings)
+        full = np.zeros(H.shape[1])
+        full[kv] = x
+        assert status[i] == (0 if ok else 1)
+        swing = np.setdiff1d(np.arange(H.shape[1]), kv)
+        assert (f[i][swing] == 0).all()
+        if iters[i] == it:
+            same += 1
+            assert rel_force_err(f[i:i + 1], full[None])[0] <= 1e-6, (i, it)
+    assert same >= 0.9 * recs.shape[0], same
+
+
+@pytest.mark.gpu
+def test_admm_reduced_tight_matches_qpoases_n20(cm):
+    solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+    solver_mod.load_library()
+    g = load_golden("n20_trot")
+    prm = golden_params(cm, g)
+    _, _, f, status, _ = _run(cm, solver_mod, g["records"], prm, dict(TIGHT, reduced=True))
+    assert (status == 0).all()
+    err = rel_force_err(f, g["q_ref"])
+    assert err.max() <= 2e-4, (err.max(), int(err.argmax()))
