@@ -15,9 +15,10 @@ sm = importlib.import_module("quad-periodic-mpc_amd.solver")
 sm.load_library()
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
-N = 10
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+REDUCED = len(sys.argv) > 3 and sys.argv[3] == "reduced"
 prm = cm.make_params(N)
-recs_np = cm.make_instances(B, N)
+recs_np = cm.make_instances(B, N, random_contact_frac=0.0) if REDUCED else cm.make_instances(B, N)
 st = torch.cuda.Stream()
 with torch.cuda.stream(st):
     s = sm.BatchSolver(prm, max_batch=B, stream=st)
@@ -28,7 +29,7 @@ with torch.cuda.stream(st):
     status = torch.empty(B, dtype=torch.uint8, device="cuda")
     iters = torch.empty(B, dtype=torch.int32, device="cuda")
     for name, kw in [("deployed", dict()), ("tight", dict(rho=1e-3, terminate=1e-4))]:
-        cfg = sm.admm_settings(**kw)
+        cfg = sm.admm_settings(reduced=REDUCED, **kw)
         s.condense(recs, H, g)
         s.admm(recs, H, g, f, status, iters, settings=cfg)
         torch.cuda.synchronize()
@@ -40,7 +41,7 @@ with torch.cuda.stream(st):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / reps
         it = iters.cpu().numpy()
-        print(json.dumps({"mode": "use_jcqp=1", "settings": name, "batch": B, "horizon": N,
+        print(json.dumps({"mode": "use_jcqp=2" if REDUCED else "use_jcqp=1", "settings": name, "batch": B, "horizon": N,
                           "qp_per_s": B / dt, "ms": dt * 1e3, "iters_mean": float(it.mean()),
                           "iters_max": int(it.max()),
                           "converged_frac": float((status.cpu().numpy() == 0).mean())}),
