@@ -2,23 +2,37 @@
 """Benchmark: QP solves/s of the fused HIP convex-MPC solver (BASELINE.json metric).
 
 One "step" = one pass of the hot path (ConvexMPCLocomotion::solveDenseMPC -> solve_mpc:
-condensation + friction-cone QP + force scatter) over one batch of synthetic instances that are
-already resident in HBM. Default workload = BASELINE config 3: batch 65536, horizon 10, fused
-condensation + QP, one GPU. With N GPUs (torchrun, one process per GPU) every rank solves its
-own 65536-instance shard (independent instances, no collective on the data path: weak scaling);
-the step time is the max over ranks.
+condensation + friction-cone QP + force scatter) over one batch of synthetic instances whose
+records are already resident in HBM when the timed region starts.
 
-  python bench.py [--gpus N --steps K --warmup W] [--batch B --horizon H] [--no-cpu-baseline]
-  python bench.py --config5     # BASELINE config 5: N = 20, estimator step + solve per step
+Workloads (BASELINE.json configs; the default follows the GPU count):
+  --config 3   (default at 1 GPU) batch 65536 per GPU, N = 10, fused condensation + QP.
+  --config 4   (default at >1 GPU) batch 262144 in total, N = 10, strong-scaled over the
+               ranks: the records live on rank 0's GPU, every step scatters them over RCCL
+               (xGMI), solves each rank's contiguous shard and gathers the forces back to rank 0,
+               software-pipelined over --chunks pieces (parallel.RootPipeline).
+  --config 2   batch 4096 per GPU, N = 10.
+  --config 5   batch 65536 per GPU, N = 20, one periodic-disturbance estimator step (LogData
+               residual, Gaussian band-pass, DFT sine fit) fused ahead of every solve.
+Instances come from the per-instance Philox generator (seed 0x5EED0000 + id), so any shard of
+ids holds exactly the instances a 1-GPU run of the same global batch holds.
 
-Rank 0 prints one JSON line.
+  python bench.py [--gpus N --steps K --warmup W] [--config C] [--batch B | --global-batch G]
+  python bench.py --gpus 2 --dry-run     # CPU/gloo plumbing check of the config-4 path
+
+With --gpus N > 1 and no torchrun environment the script relaunches itself under
+torch.distributed.run (one process per GPU) before touching any GPU. Rank 0 prints ONE JSON
+line.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,7 +42,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "QP solves/sec (N=10, 13-state, 12-force) at batch=65536; 1/2/4/8 GPU"
-FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 dense (VALU = f32 MFMA rate), MI355X_MICROARCH.md
+METRIC_C2 = "QP solves/sec (N=10) at batch=4096, 1 GPU (config 2)"
+METRIC_C5 = "QP solves/sec (N=20 + disturbance estimation, config 5) at batch=65536"
+FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (v_fma_f32 at 2 cyc/wave on SIMD-32)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -40,14 +56,26 @@ def algorithmic_flops(N: int) -> float:
     return f_cond + f_chol
 
 
-def algorithmic_bytes(N: int) -> int:
-    """compulsory HBM bytes per QP (fp32 record in, forces out)."""
-    return 64 + 48 + 48 * N + 4 * N + 4 + 48 * N
+def algorithmic_bytes(N: int, config5: bool = False) -> int:
+    """compulsory HBM bytes per QP (fp32 record in, forces out); config 5
+    adds f_est (24 B), the 400-sample history window (1600 B) and the appended sample (4 B)."""
+    b = 64 + 48 + 48 * N + 4 * N + 4 + 48 * N
+    return b + (24 + 1600 + 4 if config5 else 0)
 
 
-def cpu_baseline(prm, N: int, seed: int):
-    """Reference pipeline (fp32 dense-S condensation restated from SolverMPC.cpp + the
-    reference's qpOASES 3.2.0 built from its sources) on host cores, bounded sample."""
+def _threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(prm, N: int, config5: bool = False):
+    """The reference pipeline on the host cores (rank 0, N=1 only), bounded sample: the fp32
+    dense-S condensation restated from SolverMPC.cpp (oracle/cmpc_oracle.c) + the reference's
+    own qpOASES 3.2.0 compiled from its sources (oracle/_ref); at config 5 each instance also
+    runs the residual + estimator step first (SolverMPC.cpp:688-811, restated in C)."""
     try:
         from oracle import oracle as orc
     except Exception:
@@ -55,35 +83,117 @@ def cpu_baseline(prm, N: int, seed: int):
     if not orc.ref_available():
         return None
     cm = importlib.import_module("quad-periodic-mpc_amd")
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except AttributeError:
-        threads = os.cpu_count() or 1
-    threads = max(1, min(16, threads))
-    sample = 8192
-    recs = cm.make_instances(sample, N, seed=seed)
-    orc.ref_solve_batch(recs[:64], prm, nthreads=threads)  # warm
-    t0 = time.perf_counter()
-    orc.ref_solve_batch(recs, prm, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": sample / dt, "unit": "QP solves/s", "cores": threads, "kind": "reference",
-            "sample": f"{sample} instances of the same synthetic workload (N={N}), solve_mpc "
-                      f"equivalent per instance: fp32 dense-S condensation (SolverMPC.cpp:566-950 "
-                      f"restated, oracle/cmpc_oracle.c) + reference qpOASES 3.2.0 (setToMPC, "
-                      f"nWSR=100) built from /root/reference; {threads} std::threads; "
-                      f"{dt:.2f} s wall"}
+    threads = _threads()
+    sample = 2048 if N >= 16 else 8192
+    recs = cm.make_instances(sample, N)
+    if config5:
+        R = importlib.import_module("quad-periodic-mpc_amd.records")
+        est, logs = _config5_state(cm, R, recs, sample)
+        orc.ref_pipeline_c5_batch(recs[:32].copy(), logs[:32], est[:32].copy(), prm, 10.4,
+                                  nthreads=threads)  # warm
+        t0 = time.perf_counter()
+        orc.ref_pipeline_c5_batch(recs, logs, est, prm, 10.4, nthreads=threads)
+        dt = time.perf_counter() - t0
+        what = ("residual + band-pass/DFT estimator step (SolverMPC.cpp:688-811, restated in C) "
+                "then ")
+    else:
+        orc.ref_solve_batch(recs[:64], prm, nthreads=threads)  # warm
+        t0 = time.perf_counter()
+        orc.ref_solve_batch(recs, prm, nthreads=threads)
+        dt = time.perf_counter() - t0
+        what = ""
+    # per-call latency of the reference pipeline on one core (what one solveDenseMPC costs)
+    lat = recs[:256]
+    t1 = time.perf_counter()
+    if config5:
+        orc.ref_pipeline_c5_batch(lat.copy(), logs[:256], est[:256].copy(), prm, 10.4, nthreads=1)
+    else:
+        orc.ref_solve_batch(lat, prm, nthreads=1)
+    lat_us = (time.perf_counter() - t1) / lat.shape[0] * 1e6
+    return {"value": round(sample / dt, 1), "unit": "QP solves/s", "cores": threads,
+            "kind": "reference", "latency_us_1core": round(lat_us, 1),
+            "sample": f"{sample} instances of the same synthetic workload (N={N}), per instance "
+                      f"{what}the solve_mpc equivalent: fp32 dense-S condensation "
+                      f"(SolverMPC.cpp:566-950 restated, oracle/cmpc_oracle.c) + reference "
+                      f"qpOASES 3.2.0 (setToMPC, nWSR=100) built from /root/reference; "
+                      f"{threads} std::threads; {dt:.2f} s wall"}
 
 
-def load_traffic(path: str, N: int, batch: int):
-    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC summary."""
+def _config5_state(cm, R, recs_np, B):
+    """Estimator histories pre-filled to 400 samples (so every timed step re-estimates,
+    SolverMPC.cpp:704-707) and the previous step's LogData records."""
+    f3, tt = cm.make_disturbance(B, R.EST_WINDOW)
+    est = np.zeros((B, R.EST_WORDS), np.float32)
+    est[:, R.EST_F:R.EST_F + R.EST_WINDOW] = f3
+    est[:, R.EST_T:R.EST_T + R.EST_WINDOW] = tt[None, :]
+    est.view(np.int32)[:, R.EST_COUNT] = R.EST_WINDOW
+    est.view(np.int32)[:, R.EST_HEAD] = 0
+    logs = cm.make_logs(recs_np)
+    return est, logs
+
+
+def load_pmc(N: int, batch: int, kernel_prefix: str):
+    """HBM bytes per launch of the dominant kernel + its SQ counters from the committed
+    rocprofv3 PMC summary (profiles/pmc_summary.json, scripts/pmc_summary.py)."""
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
             d = json.load(f)
-        if d.get("horizon") == N and d.get("batch") == batch:
-            return d.get("hbm_bytes_per_launch")
     except Exception:
-        pass
-    return None
+        return None, None
+    for case in d.get("cases", [d]):
+        if case.get("horizon") != N or case.get("batch") != batch:
+            continue
+        for name, k in case.get("kernels", {}).items():
+            if kernel_prefix in name:
+                return k.get("hbm_bytes_per_launch"), k
+    return None, None
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def relaunch_distributed(nproc: int) -> int:
+    """One process per GPU under torch.distributed.run; called before any GPU work."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def abi_latency():
+    """Batch-1 latency of the drop-in single-instance ABI (setup_problem -> update_x_drag ->
+    update_solver_settings -> update_problem_data_floats -> get_solution(0..11)), measured by a
+    plain C++ caller (quad-periodic-mpc_amd/cmpc_abi_latency) in a child process."""
+    exe = os.path.join(ROOT, "quad-periodic-mpc_amd", "cmpc_abi_latency")
+    if not os.path.exists(exe):
+        return None
+    res = {}
+    for N in (10, 16):
+        try:
+            r = subprocess.run([exe, str(N), "1000"], capture_output=True, text=True, timeout=120)
+            res[f"N{N}"] = json.loads(r.stdout.strip().splitlines()[-1])
+        except Exception as e:  # diagnostics only
+            res[f"N{N}"] = repr(e)
+    return res
+
+
+def digest(t) -> str:
+    return hashlib.sha256(np.ascontiguousarray(t.cpu().numpy()).tobytes()).hexdigest()[:16]
+
+
+def plumbing_solve(N):
+    """--dry-run stand-in for the device solve (CPU ranks, no GPU): a per-instance,
+    order-sensitive function of the record, so the gathered rows show whether every instance
+    reached its rank and came back to its slot. Not a solver and never timed as one."""
+    def fn(recs, forces, status):
+        forces.copy_(recs[:, 32:32 + 12 * N] * 2.0 + recs[:, 0:1])
+        status.zero_()
+    return fn
 
 
 def main():
@@ -91,105 +201,187 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
-    ap.add_argument("--horizon", type=int, default=10)
+    ap.add_argument("--config", type=int, choices=(2, 3, 4, 5), default=None)
+    ap.add_argument("--config5", action="store_true", help="alias of --config 5")
+    ap.add_argument("--batch", type=int, default=None, help="instances per GPU (configs 2, 3, 5)")
+    ap.add_argument("--global-batch", type=int, default=None, help="total instances (config 4)")
+    ap.add_argument("--chunks", type=int, default=4, help="config-4 pipeline pieces per rank")
+    ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--random-contact-frac", type=float, default=0.25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config5", action="store_true",
-                    help="BASELINE config 5: horizon 20, one periodic-disturbance estimator step "
-                         "(residual from LogData, band-pass + DFT sine fit) fused ahead of "
-                         "every solve; histories pre-filled to 400 samples so every timed step "
-                         "runs the estimation (SolverMPC.cpp:704-707)")
+    ap.add_argument("--no-extras", action="store_true", help="skip end-to-end / solve-only legs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU ranks over gloo with a plumbing stand-in for the solve (no GPU)")
     args = ap.parse_args()
-    if args.config5:
-        args.horizon = 20
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args.gpus))
 
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    config = 5 if args.config5 else (args.config or (4 if world > 1 else 3))
+    N = args.horizon or (20 if config == 5 else 10)
+
     dist = None
-    if world > 1:
-        import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        dist = tdist
+    if args.dry_run:
+        dev = torch.device("cpu")
+        if world > 1:
+            import torch.distributed as tdist
+            tdist.init_process_group("gloo")
+            dist = tdist
     else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        # one non-default stream carries everything of this rank (copies, collectives' stream
+        # joins, the solver's launches), so the library's launches order with torch's work
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
+        if world > 1:
+            import torch.distributed as tdist
+            tdist.init_process_group("nccl", device_id=dev)
+            dist = tdist
 
     cm = importlib.import_module("quad-periodic-mpc_amd")
-    solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
-    N, B = args.horizon, args.batch
     prm = cm.make_params(N)
-    seed = 20251015 + 7919 * rank
-    recs_np = cm.make_instances(B, N, seed=seed, random_contact_frac=args.random_contact_frac)
-    recs = torch.from_numpy(recs_np).to(dev)
-    forces = torch.empty((B, 12 * N), dtype=torch.float32, device=dev)
-    status = torch.empty(B, dtype=torch.uint8, device=dev)
-    iters = torch.empty(B, dtype=torch.int32, device=dev)
-    solver = solver_mod.BatchSolver(prm, max_batch=B)
-    stream = torch.cuda.ExternalStream(solver.stream_handle, device=dev)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    def step():
-        solver.solve(recs, forces, status, iters)
+    def sync():
+        if not args.dry_run:
+            torch.cuda.synchronize()
 
-    if args.config5:
-        R = importlib.import_module("quad-periodic-mpc_amd.records")
-        f3, tt = cm.make_disturbance(B, R.EST_WINDOW, seed=seed + 5)
-        est_np = np.zeros((B, R.EST_WORDS), np.float32)
-        est_np[:, R.EST_F:R.EST_F + R.EST_WINDOW] = f3
-        est_np[:, R.EST_T:R.EST_T + R.EST_WINDOW] = tt[None, :]
-        est_np.view(np.int32)[:, R.EST_COUNT] = R.EST_WINDOW
-        est_np.view(np.int32)[:, R.EST_HEAD] = 0
-        est0 = torch.from_numpy(est_np).to(dev)
-        est = est0.clone()
-        logs = torch.from_numpy(cm.make_logs(recs_np, seed=seed + 6)).to(dev)
-        t_next = [float(tt[-1]) + prm.dt]
+    extras = {}
+    solver = None
+    if config == 4:
+        par = importlib.import_module("quad-periodic-mpc_amd.parallel")
+        G = args.global_batch or 262144
+        pipe = par.RootPipeline(prm, G, chunks=args.chunks, device=dev,
+                                solve_fn=plumbing_solve(N) if args.dry_run else None)
+        recs_root = None
+        if rank == 0:
+            recs_root = torch.from_numpy(cm.make_instances(
+                G, N, random_contact_frac=args.random_contact_frac)).to(dev)
+        B_total, B_local = G, pipe.local_batch
 
-        def step():  # noqa: F811  (config 5: estimator step, then the solve)
-            solver.estimate(est, recs, logs=logs, sim_time=t_next[0])
-            t_next[0] += prm.dt
-            solver.solve(recs, forces, status, iters)
+        def step():
+            pipe.step(recs_root)
+    else:
+        B = args.batch or (4096 if config == 2 else 65536)
+        B_total, B_local = B * world, B
+        recs_np = cm.make_instances(B, N, random_contact_frac=args.random_contact_frac,
+                                    first_id=rank * B)
+        recs = torch.from_numpy(recs_np).to(dev)
+        forces = torch.empty((B, 12 * N), dtype=torch.float32, device=dev)
+        status = torch.empty(B, dtype=torch.uint8, device=dev)
+        iters = torch.empty(B, dtype=torch.int32, device=dev)
+        if args.dry_run:
+            fn = plumbing_solve(N)
 
-    torch.cuda.synchronize()
+            def step():
+                fn(recs, forces, status)
+        else:
+            solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+            solver = solver_mod.BatchSolver(prm, max_batch=B, stream=torch.cuda.current_stream(dev))
+
+            def step():
+                solver.solve(recs, forces, status, iters)
+
+            if config == 5:
+                R = importlib.import_module("quad-periodic-mpc_amd.records")
+                est_np, logs_np = _config5_state(cm, R, recs_np, B)
+                est0 = torch.from_numpy(est_np).to(dev)
+                est = est0.clone()
+                logs = torch.from_numpy(logs_np).to(dev)
+                t_next = [10.4]
+
+                def step():  # noqa: F811  (config 5: estimator step, then the solve)
+                    solver.estimate(est, recs, logs=logs, sim_time=t_next[0])
+                    t_next[0] += prm.dt
+                    solver.solve(recs, forces, status, iters)
+
+    sync()
     for _ in range(args.warmup):
         step()
-    if args.config5:  # restart the histories at 400 samples for the timed steps
-        torch.cuda.synchronize()
+    if config == 5:  # restart the histories at 400 samples for the timed steps
+        sync()
         est.copy_(est0)
-        torch.cuda.synchronize()
-    torch.cuda.synchronize()
-    st = status.cpu().numpy()
-    if (st != 0).any():
-        print(f"[rank {rank}] WARNING: status counts {np.bincount(st)}", file=sys.stderr)
+        t_next[0] = 10.4
+    sync()
+    timed = solver
+    units_per_launch = B_local
+    if config == 4 and not args.dry_run:
+        timed = pipe._solver
+        units_per_launch = max(pipe.sizes)
+    if timed is not None:
+        timed.enable_timing(args.steps * (pipe.chunks if config == 4 else 1))
 
-    # timed region: K steps, bracketed by barrier + synchronize
-    solver.enable_timing(args.steps)
+    # ---- timed region: K steps, bracketed by barrier + synchronize on both sides ----------
     barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    sync()
     t0 = time.perf_counter()
-    ev0.record(stream)
     for _ in range(args.steps):
         step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    wall = time.perf_counter() - t0
-    gpu_ms = ev0.elapsed_time(ev1)
-    launch_ms, ovf = solver.read_timing()
-    elapsed = max(wall, gpu_ms / 1e3)
+    elapsed = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # ---- untimed extras -------------------------------------------------------------------
+    launch_ms, ovf = (timed.read_timing() if timed is not None else (np.zeros((0, 2)), 0))
+    if config == 4:
+        out_forces = pipe.forces if rank == 0 else None
+        st_local = pipe.local_status
+        if not args.no_extras:
+            barrier()
+            sync()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                pipe.solve_only()
+            sync()
+            so = time.perf_counter() - t1
+            if dist is not None:
+                t = torch.tensor([so], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                so = float(t.item())
+            extras["solve_only"] = {
+                "value": round(B_total * args.steps / so, 1), "ms_per_step": round(so / args.steps * 1e3, 4),
+                "what": "the same per-rank pieces solved with no collective (max over ranks)"}
+    else:
+        out_forces, st_local = forces, status
+        if config == 3 and not args.dry_run and not args.no_extras and world == 1:
+            # end to end: records from pinned host memory, H2D + solve + D2H per step
+            h_recs = torch.from_numpy(recs_np).pin_memory()
+            h_forces = torch.empty((B, 12 * N), dtype=torch.float32).pin_memory()
+            solver.enable_timing(0)
+            sync()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                recs.copy_(h_recs, non_blocking=True)
+                solver.solve(recs, forces, status, iters)
+                h_forces.copy_(forces, non_blocking=True)
+            sync()
+            e2e = time.perf_counter() - t1
+            extras["end_to_end"] = {
+                "value": round(B * args.steps / e2e, 1), "ms_per_step": round(e2e / args.steps * 1e3, 4),
+                "what": "H2D of the records from pinned host memory + solve + D2H of the forces "
+                        "per step (PCIe-inclusive; not `value`)"}
+    if config == 3 and not args.dry_run and not args.no_extras and world == 1:
+        extras["abi_latency"] = abi_latency()
+    status_counts = None
+    if st_local is not None:
+        sc = np.bincount(st_local.cpu().numpy(), minlength=5)
+        if dist is not None:
+            t = torch.tensor(sc.astype(np.int64), device=dev)
+            dist.all_reduce(t)
+            sc = t.cpu().numpy()
+        status_counts = {cm.STATUS_NAMES[i]: int(c) for i, c in enumerate(sc) if c}
 
     if rank != 0:
         if dist is not None:
@@ -197,34 +389,75 @@ def main():
             dist.destroy_process_group()
         return
 
-    total = B * world * args.steps
-    value = total / elapsed
+    value = B_total * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    # dominant kernel: the 64-lane size class (every instance with <= 64 stance force variables)
-    c1 = launch_ms[:, 0] if launch_ms.size else np.array([np.nan])
-    c2 = launch_ms[:, 1] if launch_ms.size else np.array([np.nan])
-    units1 = B - ovf
-    t1 = float(np.mean(c1)) * 1e-3
     fl = algorithmic_flops(N)
-    achieved = fl * units1 / t1 / 1e12 if t1 > 0 else None
-    traffic = load_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), N, B)
+    roofline = None
+    if launch_ms.size:
+        c1 = launch_ms[:, 0]
+        c2 = launch_ms[:, 1]
+        units1 = units_per_launch - ovf
+        t1 = float(np.mean(c1)) * 1e-3
+        wide = units1 < units_per_launch // 2   # at N >= 16 the wide classes carry the batch
+        if wide:
+            # whole solve (class 1 + the concurrently running wide classes) as one launch
+            t1 = float(np.mean(c1 + c2)) * 1e-3
+            units1 = units_per_launch
+        achieved = fl * units1 / t1 / 1e12 if t1 > 0 else None
+        traffic, pmc = load_pmc(N, units_per_launch, "cmpc_solve_c1_kernel" if not wide else "cmpc_solve_w")
+        roofline = {
+            "bound": "valu",
+            "achieved": round(achieved, 3) if achieved else None,
+            "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_PEAK_TFLOPS, 5) if achieved else None,
+            "traffic": traffic,
+            "kernel": ("cmpc_solve_c1_kernel (n <= 64 class, one wavefront per instance)" if not wide
+                       else "whole solve: every size class, concurrent streams"),
+            "units_per_launch": int(units1),
+            "flops_per_unit": fl,
+            "avg_launch_ms": round(t1 * 1e3, 4),
+            "class1_avg_launch_ms": round(float(np.mean(c1)), 4),
+            "tail_avg_ms": round(float(np.mean(c2)), 4),
+            "wide_class_units": int(ovf),
+            "hbm_bytes_per_unit": algorithmic_bytes(N, config == 5),
+            "hbm_gbs": round(algorithmic_bytes(N, config == 5) * value / 1e9, 3),
+            "note": "FP32 VALU roof (the path is latency/VALU-bound, not HBM: ~1300 FLOP/B). "
+                    "achieved = SURVEY §8(d) F(N) (dense reference algorithm) x instances of "
+                    "the launch / its HIP-event time on the solver stream; the kernels execute "
+                    "fewer flops (reduced n, structured condensation), so frac is speed against "
+                    "the reference's work; measured VALU utilisation is in valu_pmc",
+        }
+        if pmc:
+            roofline["valu_pmc"] = {k: pmc[k] for k in ("valu_busy", "valu_insts_per_launch",
+                                                       "lds_bank_conflict_frac", "vgpr",
+                                                       "scratch", "pmc_tag") if k in pmc}
 
     cpu = None
-    if not args.no_cpu_baseline and world == 1 and not args.config5:
-        cpu = cpu_baseline(prm, N, seed)
+    if not args.no_cpu_baseline and world == 1 and not args.dry_run:
+        cpu = cpu_baseline(prm, N, config5=(config == 5))
 
-    workload = (f"BASELINE config 3: fused condensation + friction-cone QP, horizon N={N}, "
-                f"batch={B} per GPU (A1 trot at random phase + "
-                f"{int(args.random_contact_frac * 100)}% Bernoulli(0.5) contacts), "
-                f"inputs resident in HBM")
-    metric = METRIC
-    if args.config5:
-        workload = (f"BASELINE config 5: horizon N=20, per step one batched periodic-disturbance "
+    pct = int(args.random_contact_frac * 100)
+    mix = f"A1 trot at random phase + {pct}% Bernoulli(0.5) contact tables"
+    if config == 4:
+        workload = (f"BASELINE config 4: {B_total} instances in total (N={N}, {mix}) on rank 0's "
+                    f"GPU; per step RCCL scatter over xGMI -> per-rank solve of its contiguous "
+                    f"shard ({B_local}) -> gather of the forces to rank 0, pipelined over "
+                    f"{pipe.chunks} pieces per rank")
+        metric, scaling = METRIC, "strong"
+        par_s = f"dp{world} (contiguous instance shards; RCCL scatter/gather)"
+    elif config == 5:
+        workload = (f"BASELINE config 5: horizon N={N}, per step one batched periodic-disturbance "
                     f"estimator step (LogData residual, Gaussian band-pass, DFT sine fit; "
                     f"histories at 400..{400 + args.steps} samples) fused ahead of the solve, "
-                    f"batch={B} per GPU (A1 trot + {int(args.random_contact_frac * 100)}% "
-                    f"Bernoulli(0.5) contacts)")
-        metric = "QP solves/sec (N=20 + disturbance estimation, config 5) at batch=65536"
+                    f"batch={B_local} per GPU ({mix})")
+        metric, scaling = METRIC_C5, "weak"
+        par_s = f"dp{world} (independent instance shards, no data-path collective)"
+    else:
+        workload = (f"BASELINE config {config}: fused condensation + friction-cone QP, horizon "
+                    f"N={N}, batch={B_local} per GPU ({mix}), inputs resident in HBM")
+        metric, scaling = (METRIC_C2 if config == 2 else METRIC), "weak"
+        par_s = f"dp{world} (independent instance shards, no data-path collective)"
     out = {
         "metric": metric,
         "value": round(value, 1),
@@ -234,37 +467,29 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic",
+        "data": "synthetic (per-instance Philox, seed 0x5EED0000 + id)",
         "config": {
             "workload": workload,
-            "global_batch": B * world,
-            "batch_per_gpu": B,
+            "config": config,
+            "global_batch": B_total,
+            "batch_per_gpu": B_local,
             "horizon": N,
-            "parallelism": f"dp{world} (independent instance shards, no data-path collective)",
+            "parallelism": par_s,
         },
-        "roofline": {
-            "bound": "mfma",
-            "achieved": round(achieved, 3) if achieved else None,
-            "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_PEAK_TFLOPS, 5) if achieved else None,
-            "traffic": traffic,
-            "kernel": "cmpc_solve_c1_kernel (64-lane class, one wavefront per instance)",
-            "units_per_launch": int(units1),
-            "flops_per_unit": fl,
-            "avg_launch_ms": round(float(np.mean(c1)), 4),
-            "class2_avg_launch_ms": round(float(np.mean(c2)), 4),  # 128-lane class (+ class G)
-            "class2_units_per_launch": int(ovf),
-            "note": "FP32 compute roof (f32 VALU = f32 MFMA peak); algorithmic FLOPs per SURVEY "
-                    "§8(d) F(N) (dense reference algorithm); HBM bytes/QP "
-                    f"{algorithmic_bytes(N)} -> {algorithmic_bytes(N) * value / 1e9:.2f} GB/s",
-        },
+        "roofline": roofline,
         "cpu_baseline": cpu,
+        "status_counts": status_counts,
+        "forces_digest": digest(out_forces) if out_forces is not None else None,
     }
+    if args.dry_run:
+        out["dry_run"] = "gloo CPU ranks, plumbing stand-in for the solve (not a measurement)"
+    out.update(extras)
     print(json.dumps(out), flush=True)
+    if solver is not None:
+        solver.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -206,11 +206,11 @@ typedef struct cmpc_admm_settings {
 } cmpc_admm_settings;
 /* use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): the full QP (P = qH, q = qg from
  * cmpc_batch_condense, A = fmat, l = 0, u = U_b) solved by JCQP's ADMM in fp64, one workgroup
- * per instance; horizon <= 10. With s->reduced (use_jcqp == 2, SolverMPC.cpp:984-1053) the
- * swing legs are eliminated first and any horizon is accepted while 3 x (stance foot-steps)
- * <= 120 (else status CMPC_BAD_INPUT, zeros). d_forces [batch * 12N] = the solution as float
- * (0 for eliminated variables); d_status 0 = residual below terminate, 1 = max_iter reached;
- * d_iters (may be NULL). */
+ * per instance, any horizon. With s->reduced (use_jcqp == 2, SolverMPC.cpp:984-1053) the swing
+ * legs are eliminated first. QPs of up to 120 variables keep the inverted KKT Schur complement in
+ * LDS; larger ones in per-workgroup global slabs allocated with the handle. d_forces
+ * [batch * 12N] = the solution as float (0 for eliminated variables); d_status 0 = residual
+ * below terminate, 1 = max_iter reached; d_iters (may be NULL). */
 CMPC_EXTERNC int cmpc_batch_admm(cmpc_batch* h, const float* d_records, const float* d_H,
                                  const float* d_g, int batch, const cmpc_admm_settings* s,
                                  float* d_forces, uint8_t* d_status, int32_t* d_iters);

@@ -83,6 +83,8 @@ def ref():
                                      ctypes.c_int, _d, _i, _i]
         _ref.ref_solve_batch.argtypes = [_f, ctypes.c_int, ctypes.c_void_p, _d, _i, _i, ctypes.c_int]
         _ref.oracle_condense.argtypes = [_f, ctypes.c_void_p, ctypes.POINTER(OracleCond)]
+        _ref.ref_pipeline_c5_batch.argtypes = [_f, _f, _f, ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.c_float, _d, _i, ctypes.c_int]
     return _ref
 
 
@@ -151,6 +153,23 @@ def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1):
     ref().ref_solve_batch(_fp(records), B, ctypes.byref(prm), q.ctypes.data_as(_d),
                           st.ctypes.data_as(_i), nw.ctypes.data_as(_i), int(nthreads))
     return q, st, nw
+
+
+def ref_pipeline_c5_batch(records: np.ndarray, logs: np.ndarray, est: np.ndarray, prm,
+                          sim_time: float, nthreads: int = 1):
+    """Config-5 reference pipeline, per instance: residual -> estimator step -> solve_mpc
+    (records / est updated in place) -> (q_soln [B, 12N] f64, status [B])."""
+    B = records.shape[0]
+    N = prm.horizon
+    assert records.dtype == np.float32 and records.flags["C_CONTIGUOUS"]
+    assert est.dtype == np.float32 and est.flags["C_CONTIGUOUS"]
+    logs = np.ascontiguousarray(logs, np.float32)
+    q = np.zeros((B, 12 * N))
+    st = np.zeros(B, np.int32)
+    ref().ref_pipeline_c5_batch(_fp(records), _fp(logs), _fp(est), B, ctypes.byref(prm),
+                                float(sim_time), q.ctypes.data_as(_d), st.ctypes.data_as(_i),
+                                int(nthreads))
+    return q, st
 
 
 # ---- config 5: periodic-disturbance estimation (SolverMPC.cpp:404-553, 688-811) ------------

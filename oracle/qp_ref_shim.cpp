@@ -105,3 +105,40 @@ extern "C" int ref_solve_batch(const float* records, int batch, const cmpc_param
   for (auto& t : pool) t.join();
   return 0;
 }
+
+/* Config 5: per instance the residual of the logged previous step (ConvexMPCLocomotion.cpp:639-771)
+ * and one estimator step (SolverMPC.cpp:688-798) ahead of the solve, as the reference runs them
+ * inside each solveDenseMPC -> solve_mpc call. records / est_states are updated in place
+ * (f_est(3) + use-f_est flag into the record, as qg reads them at SolverMPC.cpp:808-811). */
+extern "C" int ref_pipeline_c5_batch(float* records, const float* logs, float* est_states,
+                                     int batch, const cmpc_params* prm, float sim_time,
+                                     double* q_soln, int* status, int nthreads) {
+  const int N = prm->horizon;
+  const int stride = CMPC_REC_WORDS(N);
+  const int nv = 12 * N;
+  std::atomic<int> next(0);
+  auto worker = [&]() {
+    Scratch s(N);
+    for (;;) {
+      const int i = next.fetch_add(1);
+      if (i >= batch) break;
+      float* rec = records + (size_t)i * stride;
+      float fext[6];
+      oracle_residual(logs + (size_t)i * CMPC_LOG_WORDS, rec, fext);
+      int use = 0;
+      const float f3 = oracle_est_step(est_states + (size_t)i * CMPC_EST_WORDS, fext[3], sim_time, &use);
+      rec[CMPC_REC_FEST3] = f3;
+      const uint32_t flags = use ? 1u : 0u;
+      std::memcpy(rec + CMPC_REC_FLAGS, &flags, 4);
+      int nw = 0;
+      const int st = solve_one(rec, prm, s, q_soln ? q_soln + (size_t)i * nv : s.q_red.data(), &nw);
+      if (status) status[i] = st;
+    }
+  };
+  nthreads = std::max(1, nthreads);
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nthreads; t++) pool.emplace_back(worker);
+  worker();
+  for (auto& t : pool) t.join();
+  return 0;
+}

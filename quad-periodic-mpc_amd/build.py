@@ -19,7 +19,8 @@ LIB = os.path.join(PKG, "libcmpc_hip.so")
 OBJ = os.path.join(ROOT, "build", "obj")
 # one translation unit per kernel family so the large unrolled kernels compile in parallel
 SOURCES = ["cmpc_class1.hip", "cmpc_class2_w80.hip", "cmpc_class2_w96.hip", "cmpc_class2_w128.hip",
-           "cmpc_classg.hip", "cmpc_launch.hip", "cmpc_estimator.hip", "cmpc_assemble.hip",
+           "cmpc_wide_w80.hip", "cmpc_wide_w96.hip", "cmpc_wide_w128.hip", "cmpc_wide_w192.hip",
+           "cmpc_wide_w256.hip", "cmpc_classg.hip", "cmpc_launch.hip", "cmpc_estimator.hip", "cmpc_assemble.hip",
            "cmpc_admm.hip", "cmpc_abi.cpp"]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: the SLP pass packs adjacent row updates into v_pk_fma_f32, which ties
@@ -81,7 +82,22 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None,
     subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs,
                    check=True)
     os.replace(tmp, lib)
+    if out is None:
+        build_tools(lib)
     return lib
+
+
+def build_tools(lib: str = LIB) -> str:
+    """cmpc_abi_latency: a plain C++ caller of the reference ABI, linked against the library
+    the way the be2r controller links it (only include/cmpc_solver.h)."""
+    exe = os.path.join(PKG, "cmpc_abi_latency")
+    src = os.path.join(CSRC, "tools", "cmpc_abi_latency.cpp")
+    if not _stale(exe, [src, lib]):
+        return exe
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe + ".tmp", src, f"-L{PKG}", "-lcmpc_hip",
+                    f"-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{PKG}"], check=True)
+    os.replace(exe + ".tmp", exe)
+    return exe
 
 
 if __name__ == "__main__":

@@ -38,6 +38,10 @@ struct cmpc_batch {
   float* d_gscratch = nullptr;   // slabs of the general size class (cmpc_classg.hip)
   float* d_gauss = nullptr;      // gaussian_filter kernels of the config-5 estimator
   size_t gscratch_floats = 0;
+  double* d_admm_slabs = nullptr;  // ADMM inverses of QPs with n > 120 (cmpc_admm.hip)
+  size_t admm_slab_doubles = 0;
+  int admm_nslabs = 0;
+  float* d_admm_H = nullptr;     // condensed qH / qg staging of the single-instance ADMM path
   // staging for the host-pointer entry point (allocated lazily, sized max_batch)
   float* d_rec = nullptr;
   float* d_forces = nullptr;
@@ -93,6 +97,24 @@ static int ensure_gscratch(cmpc_batch* h) {
   return 0;
 }
 
+// the ADMM kernel keeps M^-1 of QPs with more than 120 variables in per-workgroup fp64 slabs:
+// min(max_batch, kAdmmSlabs) of (12N)^2 doubles, allocated here, never inside a solve
+static int ensure_admm_slabs(cmpc_batch* h) {
+  if (h->max_batch <= 0 || 12 * h->prm.horizon <= 120) return 0;
+  const int ns = h->max_batch < cmpc::kAdmmSlabs ? h->max_batch : cmpc::kAdmmSlabs;
+  const size_t need = (size_t)ns * cmpc::admm_slab_doubles(h->prm.horizon);
+  if (need <= h->admm_slab_doubles && h->admm_nslabs >= ns) return 0;
+  if (h->d_admm_slabs) (void)hipFree(h->d_admm_slabs);
+  h->d_admm_slabs = nullptr;
+  h->admm_slab_doubles = 0;
+  h->admm_nslabs = 0;
+  hipError_t e = hipMalloc(&h->d_admm_slabs, need * sizeof(double));
+  if (e != hipSuccess) return fail("hipMalloc(ADMM slabs)", e);
+  h->admm_slab_doubles = need;
+  h->admm_nslabs = ns;
+  return 0;
+}
+
 extern "C" int cmpc_batch_set_params(cmpc_batch* h, const cmpc_params* prm) {
   if (!h || !prm) return -1;
   if (prm->horizon < 1 || prm->horizon > CMPC_MAX_HORIZON) {
@@ -101,7 +123,8 @@ extern "C" int cmpc_batch_set_params(cmpc_batch* h, const cmpc_params* prm) {
   }
   h->prm = *prm;
   h->kp = make_kparams(*prm);
-  return ensure_gscratch(h);
+  if (int r = ensure_gscratch(h)) return r;
+  return ensure_admm_slabs(h);
 }
 
 extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int max_batch,
@@ -144,6 +167,7 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
     if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("gauss taps", e); }
   }
   if (int r = ensure_gscratch(h); r != 0) { cmpc_batch_destroy(h); return r; }
+  if (int r = ensure_admm_slabs(h); r != 0) { cmpc_batch_destroy(h); return r; }
   *out = h;
   return 0;
 }
@@ -153,6 +177,8 @@ extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (h->d_work) (void)hipFree(h->d_work);
   if (h->d_gscratch) (void)hipFree(h->d_gscratch);
   if (h->d_gauss) (void)hipFree(h->d_gauss);
+  if (h->d_admm_slabs) (void)hipFree(h->d_admm_slabs);
+  if (h->d_admm_H) (void)hipFree(h->d_admm_H);
   if (h->d_rec) (void)hipFree(h->d_rec);
   if (h->d_forces) (void)hipFree(h->d_forces);
   if (h->d_status) (void)hipFree(h->d_status);
@@ -272,9 +298,13 @@ extern "C" int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int ba
 extern "C" int cmpc_batch_admm(cmpc_batch* h, const float* d_records, const float* d_H,
                                const float* d_g, int batch, const cmpc_admm_settings* s,
                                float* d_forces, uint8_t* d_status, int32_t* d_iters) {
-  if (!h || !s || batch < 0 || batch > h->max_batch) return -1;
+  if (!h || !s || batch < 0 || batch > h->max_batch ||
+      (batch && (!d_records || !d_H || !d_g || !d_forces || !d_status))) {
+    g_last_error = "cmpc_batch_admm: bad arguments";
+    return -1;
+  }
   hipError_t e = cmpc::launch_admm(d_records, d_H, d_g, batch, h->kp, *s, d_forces, d_status,
-                                   d_iters, h->stream);
+                                   d_iters, h->d_admm_slabs, h->admm_nslabs, h->stream);
   if (e != hipSuccess) return fail("launch_admm", e);
   return 0;
 }
@@ -288,6 +318,9 @@ static int ensure_staging(cmpc_batch* h) {
     return fail("hipMalloc", e);
   if ((e = hipMalloc(&h->d_status, (size_t)h->max_batch)) != hipSuccess) return fail("hipMalloc", e);
   if ((e = hipMalloc(&h->d_iters, sizeof(int32_t) * h->max_batch)) != hipSuccess) return fail("hipMalloc", e);
+  // qH / qg of one instance at the largest horizon (the single-instance ADMM path)
+  const size_t nv = 12 * (size_t)CMPC_MAX_HORIZON;
+  if ((e = hipMalloc(&h->d_admm_H, (nv * nv + nv) * sizeof(float))) != hipSuccess) return fail("hipMalloc", e);
   return 0;
 }
 
@@ -430,10 +463,9 @@ int admm_host(cmpc_batch* h, const float* rec, int N, const cmpc_admm_settings& 
               uint8_t* st) {
   if (int r = ensure_staging(h)) return r;
   const size_t n = 12 * (size_t)N;
-  float *dH = nullptr, *dg = nullptr;
+  float* dH = h->d_admm_H;
+  float* dg = dH + n * n;
   hipError_t e;
-  if ((e = hipMalloc(&dH, (n * n + n) * sizeof(float))) != hipSuccess) return fail("hipMalloc", e);
-  dg = dH + n * n;
   int rc = 0;
   if ((e = hipMemcpyAsync(h->d_rec, rec, CMPC_REC_WORDS(N) * sizeof(float), hipMemcpyHostToDevice,
                           h->stream)) != hipSuccess)
@@ -446,7 +478,6 @@ int admm_host(cmpc_batch* h, const float* rec, int N, const cmpc_admm_settings& 
   if (!rc && (e = hipMemcpyAsync(st, h->d_status, 1, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
     rc = fail("D2H", e);
   if (!rc && (e = hipStreamSynchronize(h->stream)) != hipSuccess) rc = fail("sync", e);
-  (void)hipFree(dH);
   return rc;
 }
 
@@ -469,7 +500,10 @@ void solve_single(SingleState& s) {
   for (int i = 0; i < 12; i++) prm.weights[i] = s.weights[i];
   prm.alpha = s.alpha;
   prm.max_iter = 100;  // nWSR = 100 (SolverMPC.cpp:854)
-  cmpc_batch_set_params(s.h, &prm);
+  if (std::memcmp(&prm, &s.h->prm, sizeof(prm)) != 0 && cmpc_batch_set_params(s.h, &prm) != 0) {
+    std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
+    return;
+  }
 
   estimator_step(s);
 
@@ -491,14 +525,19 @@ void solve_single(SingleState& s) {
 
   std::vector<float> forces(12 * N);
   uint8_t st = 0;
-  if ((s.use_jcqp == 1 && N <= 10) || s.use_jcqp == 2) {
+  if (s.use_jcqp == 1 || s.use_jcqp == 2) {
     // use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): ADMM over the full QP; use_jcqp == 2
-    // (:984-1053): over the reduced one. The reference keeps JCQP's solution whatever the
-    // residual, so no failure message
+    // (:984-1053): over the reduced one; any horizon (QPs beyond 120 variables keep M^-1 in a
+    // global slab). The reference keeps JCQP's solution whatever the residual (status 0 or 1),
+    // so no failure message for those
     cmpc_admm_settings as{s.max_iterations, s.rho, s.sigma, s.solver_alpha, s.terminate,
                           s.use_jcqp == 2 ? 1 : 0};
     if (admm_host(s.h, rec.data(), N, as, forces.data(), &st) != 0) {
       std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
+      return;
+    }
+    if (st != 0 && st != 1) {  // not solved at all: keep the previous solution, as qpOASES' failure
+      std::printf("failed to solve!\n");
       return;
     }
     s.q_soln.assign(12 * N, 0.0);
@@ -539,7 +578,7 @@ extern "C" void update_solver_settings(int max_iter, double rho, double sigma, d
   g.solver_alpha = solver_alpha;
   g.terminate = terminate;
   g.use_jcqp = use_jcqp > 1.5 ? 2 : (use_jcqp > 0.5 ? 1 : 0);
-  // use_jcqp == 1 / 2 run the ADMM kernel (full QP for N <= 10 / reduced QP)
+  // use_jcqp == 1 / 2 run the ADMM kernel (full / reduced QP)
 }
 
 extern "C" void update_problem_data_floats(float* p, float* v, float* q, float* w, float* r, float roll,

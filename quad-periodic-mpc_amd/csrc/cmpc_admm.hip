@@ -11,8 +11,11 @@
 // LDS by Gauss-Jordan (SPD, no pivoting); per iteration xt = M^-1 (sigma xp - q + A'(rho zp - y))
 // and zt = A xt, which is what solveLinearSystem's "step!" line produces. stepX / stepZ / stepY
 // and the every-10-iterations residual (p + d) / 4 against _zPrev follow QpProblem.cpp:306-381.
-// M (n x n doubles) is resident in LDS, n <= 120: the full QP up to N = 10; the reduced one
-// (use_jcqp == 2) while 3 x (stance foot-steps) <= 120, e.g. trot up to N = 20.
+// M (n x n doubles) is resident in LDS while n <= 120 (the full QP up to N = 10; the reduced one
+// (use_jcqp == 2) while 3 x (stance foot-steps) <= 120, e.g. trot up to N = 20). Larger problems
+// (the full QP at N = 11..24, the reference's deployed N = 16 included; reduced QPs with more
+// stance foot-steps) keep M in a per-workgroup fp64 slab in global memory (L2-resident: 295 KB at
+// n = 192) with the same arithmetic, over a persistent grid of slabs (cmpc_admm_gm_kernel).
 #include "cmpc_kernels.h"
 
 namespace cmpc {
@@ -55,19 +58,52 @@ __device__ __forceinline__ double block_max(double v, double* red) {
   return r;
 }
 
-__global__ void __launch_bounds__(kAdmmThreads)
-cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
-                 const float* __restrict__ gg, AdmmParams ap, float* __restrict__ forces,
-                 uint8_t* __restrict__ status, int32_t* __restrict__ iters) {
-  __shared__ double M[kNV * kNV];
-  __shared__ double sx[2][kNV], sz[2][kNV > kNC ? kNV : kNC];
-  __shared__ double sy[kNC], sq[kNV], srhs[kNV], sxt[kNV], srho[kNC], su[kNC];
-  __shared__ double red[kAdmmThreads];
-  __shared__ int smap[4 * CMPC_MAX_HORIZON];   // compact foot-step -> foot-step (variables 3b..)
-  __shared__ int sinv[4 * CMPC_MAX_HORIZON];   // foot-step -> compact, -1 if eliminated
-  __shared__ int snb;
+// Barrier over the workgroup that also orders M's traffic: with M in a global slab the
+// workgroup-scope fences of __syncthreads do not wait for this wave's global stores nor refresh
+// the CU's L1, so the agent-scope release (s_waitcnt vmcnt(0), L2 write-back) and acquire (L1
+// invalidate) around it publish every store of M to the other waves of the workgroup.
+template <bool GM>
+__device__ __forceinline__ void msync() {
+  if constexpr (GM) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  } else {
+    __syncthreads();
+  }
+}
+
+template <int NV, int NC>
+struct AdmmShared {
+  double sx[2][NV], sz[2][NV > NC ? NV : NC];
+  double sy[NC], sq[NV], srhs[NV], sxt[NV], srho[NC], su[NC];
+  double red[kAdmmThreads];
+  int smap[4 * CMPC_MAX_HORIZON];   // compact foot-step -> foot-step (variables 3b..)
+  int sinv[4 * CMPC_MAX_HORIZON];   // foot-step -> compact, -1 if eliminated
+  int snb;
+};
+
+// One instance by one workgroup. M: the n x n Schur complement / its inverse, in LDS (n <= 120)
+// or in this workgroup's global slab. Returns false (nothing written) when the instance's n is
+// outside [n_lo, NV] — another launch owns it.
+template <int NV, int NC, bool GM>
+__device__ bool admm_solve(const float* __restrict__ recs, const float* __restrict__ gH,
+                           const float* __restrict__ gg, const AdmmParams& ap,
+                           float* __restrict__ forces, uint8_t* __restrict__ status,
+                           int32_t* __restrict__ iters, int inst, double* __restrict__ M,
+                           AdmmShared<NV, NC>& sh, int n_lo) {
+  double(&sx)[2][NV] = sh.sx;
+  auto& sz = sh.sz;
+  double* sy = sh.sy;
+  double* sq = sh.sq;
+  double* srhs = sh.srhs;
+  double* sxt = sh.sxt;
+  double* srho = sh.srho;
+  double* su = sh.su;
+  double* red = sh.red;
+  int* smap = sh.smap;
+  int* sinv = sh.sinv;
   const int t = threadIdx.x;
-  const int inst = blockIdx.x;
   const int nf = 12 * ap.N;                    // full variable count = qH stride
   const float* H = gH + (size_t)inst * nf * nf;
   const float* rec = recs + (size_t)inst * ap.rec_words;
@@ -75,6 +111,7 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
   const double mi = (double)ap.mu_inv;
   // Elimination (reduced mode): a foot-step whose fz row has lb = ub = 0 (gait 0) loses its three
   // variables and five rows; the kept ones stay in order (SolverMPC.cpp:859-950)
+  __syncthreads();   // the previous instance of a persistent workgroup is done with sh
   if (t == 0) {
     int c = 0;
     for (int b = 0; b < 4 * ap.N; ++b) {
@@ -82,18 +119,11 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
       sinv[b] = keep ? c : -1;
       if (keep) smap[c++] = b;
     }
-    snb = c;
+    sh.snb = c;
   }
   __syncthreads();
-  const int nb = snb, n = 3 * nb, m = 5 * nb;
-  if (n > kNV) {               // reduced problem still too large for the LDS-resident inverse
-    for (int v = t; v < nf; v += kAdmmThreads) forces[(size_t)inst * nf + v] = 0.f;
-    if (t == 0) {
-      status[inst] = CMPC_BAD_INPUT;
-      if (iters) iters[inst] = 0;
-    }
-    return;
-  }
+  const int nb = sh.snb, n = 3 * nb, m = 5 * nb;
+  if (n > NV || n < n_lo) return false;   // another size class owns this instance
 
   // ---- setup: P + sigma I, q, u, rho; cold start (QpProblem.cpp:9-20) ----
   for (int e = t; e < n * n; e += kAdmmThreads) {
@@ -120,7 +150,7 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
     sz[0][r] = 0.0;
     sz[1][r] = 0.0;
   }
-  __syncthreads();
+  msync<GM>();
   // A' diag(rho) A: block-diagonal, 3x3 per foot-step b (variables 3b..3b+2, rows 5b..5b+4)
   for (int e = t; e < 9 * (n / 3); e += kAdmmThreads) {
     const int b = e / 9, a0 = (e - 9 * b) / 3, a1 = e - 9 * b - 3 * a0;
@@ -128,23 +158,23 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
     for (int k = 0; k < 5; ++k) s += srho[5 * b + k] * fcoef(k, a0, mi) * fcoef(k, a1, mi);
     M[(3 * b + a0) * n + 3 * b + a1] += s;
   }
-  __syncthreads();
+  msync<GM>();
 
   // ---- Gauss-Jordan inverse in place (SPD: no pivoting) ----
   for (int k = 0; k < n; ++k) {
     const double piv = 1.0 / M[k * n + k];
     for (int j = t; j < n; j += kAdmmThreads)
       if (j != k) M[k * n + j] *= piv;
-    __syncthreads();
+    msync<GM>();
     for (int e = t; e < n * n; e += kAdmmThreads) {
       const int i = e / n, j = e - i * n;
       if (i != k && j != k) M[e] -= M[i * n + k] * M[k * n + j];
     }
-    __syncthreads();
+    msync<GM>();
     for (int i = t; i < n; i += kAdmmThreads)
       if (i != k) M[i * n + k] *= -piv;
     if (t == 0) M[k * n + k] = piv;
-    __syncthreads();
+    msync<GM>();
   }
 
   // ---- ADMM iterations (runFromDense, QpProblem.cpp:165-225) ----
@@ -171,8 +201,11 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
     // xt = M^-1 rhs: two adjacent lanes per row, each half of the columns with four
     // independent accumulators (the LDS reads pipeline instead of one serial FMA chain), then a
     // lane-pair shuffle; M^-1 is symmetric, so lanes of a row read down a column
-    if (t < 2 * n) {
-      const int i = t >> 1, h = t & 1, half = n >> 1;   // n = 3 x kept foot-steps: may be odd
+    // (rows beyond 128, the global-slab sizes, take further passes of the 256 lanes)
+    for (int b0 = 0; b0 < 2 * n; b0 += kAdmmThreads) {
+      const int tt = b0 + t;
+      if (tt >= 2 * n) break;
+      const int i = tt >> 1, h = tt & 1, half = n >> 1;   // n = 3 x kept foot-steps: may be odd
       const int j0 = h ? half : 0, j1 = h ? n : half;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       int j = j0;
@@ -247,21 +280,56 @@ cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
     status[inst] = st;
     if (iters) iters[inst] = it_done;
   }
+  return true;
+}
+
+__global__ void __launch_bounds__(kAdmmThreads)
+cmpc_admm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
+                 const float* __restrict__ gg, AdmmParams ap, float* __restrict__ forces,
+                 uint8_t* __restrict__ status, int32_t* __restrict__ iters) {
+  __shared__ double M[kNV * kNV];
+  __shared__ AdmmShared<kNV, kNC> sh;
+  admm_solve<kNV, kNC, false>(recs, gH, gg, ap, forces, status, iters, blockIdx.x, M, sh, 0);
+}
+
+// n > 120: M in a global fp64 slab per workgroup, persistent over the batch
+constexpr int kGNV = 12 * CMPC_MAX_HORIZON;
+constexpr int kGNC = 20 * CMPC_MAX_HORIZON;
+__global__ void __launch_bounds__(kAdmmThreads)
+cmpc_admm_gm_kernel(const float* __restrict__ recs, const float* __restrict__ gH,
+                    const float* __restrict__ gg, AdmmParams ap, float* __restrict__ forces,
+                    uint8_t* __restrict__ status, int32_t* __restrict__ iters, int batch,
+                    double* __restrict__ slabs) {
+  __shared__ AdmmShared<kGNV, kGNC> sh;
+  const int nf = 12 * ap.N;
+  double* M = slabs + (size_t)blockIdx.x * nf * nf;
+  for (int inst = blockIdx.x; inst < batch; inst += gridDim.x)
+    admm_solve<kGNV, kGNC, true>(recs, gH, gg, ap, forces, status, iters, inst, M, sh, kNV + 1);
 }
 
 }  // namespace
 
+size_t admm_slab_doubles(int horizon) { return (size_t)144 * horizon * horizon; }
+
 hipError_t launch_admm(const float* d_recs, const float* d_H, const float* d_g, int batch,
                        const KParams& P, const cmpc_admm_settings& s, float* d_forces,
-                       uint8_t* d_status, int32_t* d_iters, hipStream_t stream) {
-  if (P.N < 1 || P.N > (s.reduced ? CMPC_MAX_HORIZON : kAdmmMaxN) || s.max_iter < 1 ||
-      !(s.rho > 0) || !(s.alpha > 0))
+                       uint8_t* d_status, int32_t* d_iters, double* d_slabs, int nslabs,
+                       hipStream_t stream) {
+  if (P.N < 1 || P.N > CMPC_MAX_HORIZON || s.max_iter < 1 || !(s.rho > 0) || !(s.alpha > 0))
     return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
   AdmmParams ap{s.rho, s.sigma, s.alpha, s.terminate, s.max_iter, P.N, P.rec_words, P.mu_inv,
                 P.f_max, s.reduced ? 1 : 0};
-  hipLaunchKernelGGL(cmpc_admm_kernel, dim3(batch), dim3(kAdmmThreads), 0, stream, d_recs, d_H,
-                     d_g, ap, d_forces, d_status, d_iters);
+  const bool small_possible = s.reduced || P.N <= kAdmmMaxN;
+  const bool large_possible = 12 * P.N > kNV;
+  if (large_possible && (!d_slabs || nslabs < 1)) return hipErrorInvalidValue;
+  if (small_possible)
+    hipLaunchKernelGGL(cmpc_admm_kernel, dim3(batch), dim3(kAdmmThreads), 0, stream, d_recs, d_H,
+                       d_g, ap, d_forces, d_status, d_iters);
+  if (large_possible)
+    hipLaunchKernelGGL(cmpc_admm_gm_kernel, dim3(batch < nslabs ? batch : nslabs),
+                       dim3(kAdmmThreads), 0, stream, d_recs, d_H, d_g, ap, d_forces, d_status,
+                       d_iters, batch, d_slabs);
   return hipGetLastError();
 }
 

@@ -30,9 +30,10 @@ struct LocoParams {
 };
 
 // Scratch ints needed by launch_solve for max_batch instances.
-// d_work: [0] instances with n > 64, [1..4] lengths of the class lists (rows of 80, 96, 128,
-// general), [8 ..) the four lists of max_batch entries each
-inline size_t work_ints(int max_batch) { return 8 + 4 * (size_t)max_batch; }
+// d_work: [0] instances with n > 64, [1..6] lengths of the class lists (wide classes of 80, 96,
+// 128, 192, 256 columns, general), [8 ..) the six lists of max_batch entries each
+constexpr int kLists = 6;
+inline size_t work_ints(int max_batch) { return 8 + kLists * (size_t)max_batch; }
 // Side streams and events of one handle: the wider size classes run concurrently with class 1
 // (they are latency-bound: few instances, long serial solves). Two side streams: with the
 // handle's own stream that is three of the four hardware queues a process gets by default
@@ -67,6 +68,17 @@ CMPC_DECL_CLASS2(80)
 CMPC_DECL_CLASS2(96)
 CMPC_DECL_CLASS2(128)
 #undef CMPC_DECL_CLASS2
+// wide classes, two lanes per row, NV/32 wavefronts (cmpc_wide_w{80,96,128,192,256}.hip)
+#define CMPC_DECL_WIDE(W)                                                                          \
+  hipError_t launch_wide_w##W(const float* d_recs, const KParams& P, float* d_forces,             \
+                              uint8_t* d_status, int32_t* d_iters, const int* in_list,            \
+                              const int* in_count, int grid, hipStream_t stream);
+CMPC_DECL_WIDE(80)
+CMPC_DECL_WIDE(96)
+CMPC_DECL_WIDE(128)
+CMPC_DECL_WIDE(192)
+CMPC_DECL_WIDE(256)
+#undef CMPC_DECL_WIDE
 hipError_t launch_classg(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          float* scratch, int grid, hipStream_t stream);
@@ -90,9 +102,14 @@ hipError_t launch_rollout(float* d_loco, const float* d_recs, const float* d_for
 hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
                            float* scratch, int grid, hipStream_t stream);
 
-// use_jcqp == 1: batched JCQP ADMM over the full condensed QP (cmpc_admm.hip)
+// use_jcqp == 1 / 2: batched JCQP ADMM over the full / reduced condensed QP (cmpc_admm.hip).
+// Instances whose QP has n > 120 variables run on nslabs persistent workgroups with M in
+// d_slabs (nslabs * admm_slab_doubles(N) doubles); may be NULL when no such instance can occur.
+size_t admm_slab_doubles(int horizon);
+constexpr int kAdmmSlabs = 512;
 hipError_t launch_admm(const float* d_recs, const float* d_H, const float* d_g, int batch,
                        const KParams& P, const cmpc_admm_settings& s, float* d_forces,
-                       uint8_t* d_status, int32_t* d_iters, hipStream_t stream);
+                       uint8_t* d_status, int32_t* d_iters, double* d_slabs, int nslabs,
+                       hipStream_t stream);
 
 }  // namespace cmpc

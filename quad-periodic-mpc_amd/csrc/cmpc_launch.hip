@@ -2,11 +2,13 @@
 //   classify (this file): n = 3 x stance foot-steps per instance (SolverMPC.cpp:869-894), the
 //     instances with n > 64 appended to the list of their class;
 //   class 1 (cmpc_class1.hip): every instance, one wavefront each; exits when n > 64;
-//   class 2 (cmpc_class2.h), 128-lane workgroups, rows of 80 / 96 / 128, and class G
-//     (cmpc_classg.hip, any n): each over its own list, on two side streams forked after
-//     classify (rows of 80, then G, on one; 96, 128 on the other), so they run concurrently
-//     with class 1 and with each other (at N = 10 they are latency-bound: few, long solves; at
-//     N = 20 the 128-row class and G carry most of the batch).
+//   wide classes (cmpc_wide.h: two lanes per row, NV/32 wavefronts; NV = 80, 96, 128, 192, 256)
+//     and class G (cmpc_classg.hip, any n, global slabs) each over its own list, on two side
+//     streams forked after classify, so they run concurrently with class 1 and with each
+//     other. At N = 10 they are a latency-bound tail (few, long solves); at N = 16..20 the 128-
+//     and 192-column classes carry the batch and run side by side on the two streams.
+//   -DCMPC_LEGACY_C2 builds the round-1 arrangement instead (one lane per row, 2-wavefront
+//     classes of 80 / 96 / 128 columns, G above 128) for A/B measurements.
 #include "cmpc_kernels.h"
 
 namespace cmpc {
@@ -34,13 +36,18 @@ __global__ __launch_bounds__(256) void cmpc_classify_kernel(const float* __restr
       }
     }
     const int n = 3 * nfs;
-    cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : 3;
+#ifdef CMPC_LEGACY_C2
+    cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : 5;
+#else
+    cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : (n <= 192) ? 3
+        : (n <= 256) ? 4 : 5;
+#endif
   }
   const unsigned long long any = __ballot(cls >= 0);
   if (any == 0ull) return;
   if (lane == 0) atomicAdd(&cnt[0], __popcll(any));
 #pragma unroll
-  for (int c = 0; c < 4; c++) {
+  for (int c = 0; c < kLists; c++) {
     const unsigned long long m = __ballot(cls == c);
     if (m == 0ull) continue;
     const int leader = __ffsll((long long)m) - 1;
@@ -58,14 +65,13 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                         float* d_gscratch, hipStream_t stream, const LaunchCtx& ctx,
                         hipEvent_t* ev) {
   int* cnt = d_work;
-  int* list[4];
-  for (int j = 0; j < 4; j++) list[j] = d_work + 8 + (size_t)j * max_batch;
+  int* list[kLists];
+  for (int j = 0; j < kLists; j++) list[j] = d_work + 8 + (size_t)j * max_batch;
   hipError_t e = hipMemsetAsync(d_work, 0, 8 * sizeof(int), stream);
   if (e != hipSuccess) return e;
   if (batch <= 0) return hipSuccess;
   const int n_max = 12 * P.N;  // a class no instance of this horizon can reach is not launched
-  const bool wide[4] = {n_max > 64, n_max > 80, n_max > 96, n_max > 128};
-  if (wide[0]) {
+  if (n_max > 64) {
     hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_recs,
                        batch, P, cnt, d_work + 8, max_batch);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -74,18 +80,40 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       if ((e = hipStreamWaitEvent(ctx.side[s], ctx.fork, 0)) != hipSuccess) return e;
     // one workgroup per possible list entry (the lengths are only known on the device);
     // surplus workgroups exit after one load
+#ifdef CMPC_LEGACY_C2
     if ((e = launch_class2_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], nullptr,
                                nullptr, batch, ctx.side[0])) != hipSuccess)
       return e;
-    if (wide[1] && (e = launch_class2_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2],
-                                          nullptr, nullptr, batch, ctx.side[1])) != hipSuccess)
+    if (n_max > 80 && (e = launch_class2_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2],
+                                             nullptr, nullptr, batch, ctx.side[1])) != hipSuccess)
       return e;
-    if (wide[2] && (e = launch_class2_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
-                                           nullptr, nullptr, batch, ctx.side[1])) != hipSuccess)
+    if (n_max > 96 && (e = launch_class2_w128(d_recs, P, d_forces, d_status, d_iters, list[2],
+                                              &cnt[3], nullptr, nullptr, batch, ctx.side[1])) != hipSuccess)
       return e;
-    if (wide[3] && (e = launch_classg(d_recs, batch, P, d_forces, d_status, d_iters, list[3],
-                                      &cnt[4], d_gscratch, classg_grid(max_batch),
-                                      ctx.side[0])) != hipSuccess)
+    const bool g_possible = n_max > 128;
+#else
+    // side 0: 80, 128, 256; side 1: 96, 192 (at N = 20 the 128- and 192-column classes, which
+    // carry the batch, run side by side)
+    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], batch,
+                             ctx.side[0])) != hipSuccess)
+      return e;
+    if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2],
+                                           batch, ctx.side[1])) != hipSuccess)
+      return e;
+    if (n_max > 96 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
+                                            batch, ctx.side[0])) != hipSuccess)
+      return e;
+    if (n_max > 128 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4],
+                                             batch, ctx.side[1])) != hipSuccess)
+      return e;
+    if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5],
+                                             batch, ctx.side[0])) != hipSuccess)
+      return e;
+    const bool g_possible = n_max > 256;
+#endif
+    if (g_possible && (e = launch_classg(d_recs, batch, P, d_forces, d_status, d_iters, list[5],
+                                         &cnt[6], d_gscratch, classg_grid(max_batch),
+                                         ctx.side[1])) != hipSuccess)
       return e;
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
@@ -93,7 +121,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                     nullptr, batch, stream);
   if (e != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
-  if (wide[0]) {
+  if (n_max > 64) {
     for (int s = 0; s < kSideStreams; s++) {
       if ((e = hipEventRecord(ctx.join[s], ctx.side[s])) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(stream, ctx.join[s], 0)) != hipSuccess) return e;

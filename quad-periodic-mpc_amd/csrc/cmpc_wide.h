@@ -1,0 +1,771 @@
+// cmpc_wide.h — the wide size classes (template over the row width NV = 80, 96, 128, 192, 256):
+// fused condensation + friction-cone QP for instances with more than 64 reduced force variables
+// (random contact tables at N = 10; trot at N >= 11, the deployed N = 16 and config 5's N = 20;
+// all-stance tables), over the classify pass's list of the class.
+//
+// Same computation as cmpc_class1.hip — one call of the reference's solve_mpc()
+// (be2r_cmpc_unitree/src/controllers/convexMPC/SolverMPC.cpp:566-982): stance table + swing
+// elimination, model + closed-form c2qp, structured condensation of the reduced qH / qg,
+// bordered Cholesky, J = L^-T, Goldfarb-Idnani dual active set on the friction pyramids
+// (qpOASES QProblem::init in the reference, :955-969), scatter to q_soln.
+//
+// MI355X mapping: TWO lanes per matrix row, NV/32 wavefronts per instance.
+//   * thread t: wave w = t / 64, lane l = t % 64, half h = l / 32, row r = 32 w + l % 32; the
+//     two lanes of a row are partners across the wave's halves (v_permlane32_swap exchanges and
+//     sums their registers in one VALU op, no LDS);
+//   * each lane holds NV/2 columns of its row in registers (64 at NV = 128, against 128 when one
+//     lane owns a whole row: no spills, <= 128 VGPRs, four waves per SIMD to hide the LDS and
+//     barrier latency of the factorisation);
+//   * factorisation phases (Cholesky, J = L^-T): half h owns columns c = 2j + h (interleaved, so
+//     both halves keep work to the end). Each published pivot row of the factor is stored in LDS
+//     as its even- and odd-column segments from column 2 j0(k) on, so every half reads its own
+//     columns as contiguous ds_read_b128;
+//   * active-set phase: J's columns are relabelled l = h NV/2 + j (any column permutation of
+//     J keeps J J' = H^-1), so the Givens chains of a drop run along one lane's registers; only
+//     an active set larger than NV/2 crosses between the halves (one exchange at the seam);
+//   * the QP's triangular factor R is explicit, packed by columns in LDS, maintained by
+//     wavefront 0 with readlane chains (RQ = NV/64 active-set positions per lane).
+// Everything is fp32 (the reference condenses in fp32: common_types.h:14).
+#pragma once
+#include "cmpc_common.h"
+
+#ifndef CMPC_WIDE_WAVES_PER_EU
+#define CMPC_WIDE_WAVES_PER_EU 3
+#endif
+// hard VGPR cap per row width (0: none); 128 = four waves per SIMD
+#ifndef CMPC_WIDE_VGPR_CAP
+#define CMPC_WIDE_VGPR_CAP 0
+#endif
+
+namespace cmpc {
+namespace {
+
+constexpr int kNoneW = 0x7fffffff;
+
+template <int NV>
+struct WGeo {
+  static_assert(NV % 16 == 0, "row width");
+  static constexpr int NH = NV / 2;             // columns per lane
+  static constexpr int NW = (NV + 31) / 32;     // wavefronts (32 rows each)
+  static constexpr int NT = 64 * NW;            // threads
+  static constexpr int RQ = (NV + 63) / 64;     // active-set positions per lane of wave 0
+  static constexpr int HOFF = NH + 8;           // half 1's base in logical-order LDS vectors
+  static constexpr int VL = HOFF + NH;
+  // condensation: H as packed upper rows (row r holds columns [r & ~3, NV), 16-B aligned)
+  static constexpr int NG = NV / 4;
+  static constexpr int PSZ_H = 4 * NG * NV - 8 * NG * (NG - 1);
+  __host__ __device__ static constexpr int prow(int r) {
+    return 4 * (r >> 2) * NV - 8 * (r >> 2) * ((r >> 2) - 1) + (r & 3) * (NV - 4 * (r >> 2));
+  }
+  __host__ __device__ static constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+  // factor rows: row k = even-column segment then odd-column segment, columns 2 j0(k) + h on
+  __host__ __device__ static constexpr int j0(int k) { return (k >> 1) & ~3; }
+  __host__ __device__ static constexpr int seg(int k) {  // segment stride (words)
+    return (NH - j0(k)) + (((NH - j0(k)) % 64 == 0) ? 4 : 0);
+  }
+  __host__ __device__ static constexpr int fbase(int k) {
+    int b = 0;
+    for (int i = 0; i < k; i++) b += 2 * seg(i);
+    return b;
+  }
+  static constexpr int PSZ_F = fbase(NV);
+  static constexpr int PSZ_R = NV * (NV + 1) / 2;
+  static constexpr int mx(int a, int b) { return a > b ? a : b; }
+  static constexpr int PSZ = mx(mx(PSZ_H, PSZ_F), PSZ_R);
+};
+
+// logical-order LDS index (half 1 starts HOFF words in: the halves' ds_read_b128 never share a bank)
+template <int NV>
+__device__ __forceinline__ int lidx(int l) {
+  return l + ((l >= WGeo<NV>::NH) ? (WGeo<NV>::HOFF - WGeo<NV>::NH) : 0);
+}
+__device__ __forceinline__ int rcol_w(int j) { return (j * (j + 1)) >> 1; }
+
+constexpr int W_OFF_E = 0;
+constexpr int W_OFF_ZE = W_OFF_E + 16 * MAXN;
+constexpr int W_OFF_REC = W_OFF_ZE + 16 * MAXN;   // LDS copy of the instance record
+
+template <int NV>
+struct SharedW {
+  using G = WGeo<NV>;
+  alignas(16) float P[G::PSZ];
+  float BdtT[12][16];
+  float ibuf[NV];             // 1 / sqrt(d_k) of pivot k
+  float gbuf[NV];             // gradient border of pivot row k
+  float ybuf[2][G::NH + 4];   // y = L^-1 g, de-interleaved: ybuf[h][j] = y[2 j + h]
+  float vbuf[G::VL];          // masked d, then the Householder vector (logical order)
+  float bufA[G::VL], bufB[G::VL];  // J rows ia, iz (logical order)
+  float dfull[NV];            // d = J' n+ (logical index)
+  float xs[NV];               // x by reduced variable
+  float cs[2 * NV + 8];       // Givens (c, s) per logical column pair (half 1 at +4 words)
+  float redf[16];
+  int redi[16];
+  float sub[4 * MAXN];        // ub of each stance foot-step (gait * f_max)
+  int sfs[4 * MAXN];          // stance foot-step ids, in order
+  int blkbase[MAXN + 2];      // first reduced variable of each horizon step
+  unsigned char varblk[G::NT], varcol[G::NT];
+  unsigned char stance[4 * MAXN];
+  unsigned char cflag[2 * NV + 8];  // active flag per constraint id (6 per stance foot-step)
+};
+static_assert(W_OFF_REC + CMPC_REC_WORDS(MAXN) <= WGeo<80>::PSZ, "prep scratch must fit in P");
+
+__device__ __forceinline__ void wbar() { __syncthreads(); }
+__device__ __forceinline__ void wlsync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ float wdiv(float a, float b) { return a * fast_rcp(b); }
+
+// partner exchange across the halves of the wavefront: returns (own + partner)
+__device__ __forceinline__ float pair_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// the partner lane's value (lane l ^ 32)
+__device__ __forceinline__ float pair_other(float x, int h) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(h ? r[0] : r[1]);
+}
+
+template <int M>
+__device__ __forceinline__ void wpin(float (&x)[M]) {
+#pragma unroll
+  for (int c = 0; c < M; c++) asm volatile("" : "+v"(x[c]));
+}
+
+#define CMPC_WSWEEP_FENCE(c)                                 \
+  do {                                                       \
+    if (((c) & 15) == 12) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
+// readlane of position i (0 <= i < 64 RQ) of a per-lane array of RQ registers (i uniform)
+template <int RQ>
+__device__ __forceinline__ float rl_pos(const float (&a)[RQ], int i) {
+  float x = 0.f;
+  static_for<0, RQ>([&](auto M) {
+    constexpr int m = decltype(M)::value;
+    if ((i >> 6) == m) x = rl(a[m], i & 63);
+  });
+  return x;
+}
+template <int RQ>
+__device__ __forceinline__ int rli_pos(const int (&a)[RQ], int i) {
+  int x = 0;
+  static_for<0, RQ>([&](auto M) {
+    constexpr int m = decltype(M)::value;
+    if ((i >> 6) == m) x = rli(a[m], i & 63);
+  });
+  return x;
+}
+
+template <int NV>
+__device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KParams& P,
+                                        SharedW<NV>& sh, float* __restrict__ fout,
+                                        uint8_t* __restrict__ st_out, int32_t* __restrict__ it_out) {
+  using G = WGeo<NV>;
+  constexpr int NH = G::NH;
+  constexpr int RQ = G::RQ;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int h = lane >> 5;
+  const int r = 32 * wave + (lane & 31);   // matrix row of this lane (rows >= NV: idle lanes)
+  const int N = P.N;
+  // ---- stage the record in LDS (16-B loads, one HBM round trip for the whole prep)
+  {
+    const float4* src = reinterpret_cast<const float4*>(rec);
+    float4* dst = reinterpret_cast<float4*>(&sh.P[W_OFF_REC]);
+    for (int i = t; i < (P.rec_words >> 2); i += G::NT) dst[i] = src[i];
+  }
+  wbar();
+  const float* srec = &sh.P[W_OFF_REC];
+  // ---- stance table + elimination (SolverMPC.cpp:869-894); every wave compacts, wave 0 stores
+  const unsigned char* gait = reinterpret_cast<const unsigned char*>(srec + CMPC_REC_HDR + 12 * N);
+  int nfs = 0;
+  unsigned long long msk0 = 0ull, msk1 = 0ull;
+  for (int c0 = 0; c0 < 4 * N; c0 += 64) {
+    const int s = c0 + lane;
+    float ub = 0.f;
+    bool f = false;
+    if (s < 4 * N) {
+      ub = (float)gait[s] * P.f_max;
+      f = !(ub < 0.01f && ub > -0.01f);
+      if (wave == 0) sh.stance[s] = f ? 1 : 0;
+    }
+    const unsigned long long m = __ballot(f);
+    if (c0 == 0) msk0 = m; else msk1 = m;
+    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (f && wave == 0) {
+      sh.sfs[nfs + pre] = s;
+      sh.sub[nfs + pre] = ub;
+    }
+    nfs += __popcll(m);
+  }
+  const int n = 3 * nfs;
+  if (n > NV) {  // not this class's instance (classify guarantees it never happens)
+    if (t == 0) { st_out[0] = CMPC_BAD_INPUT; if (it_out) it_out[0] = 0; }
+    return;
+  }
+  wbar();
+  {
+    int kb = 0, kc = 0;
+    if (t < n) {
+      const int fs = sh.sfs[t / 3];
+      kb = fs >> 2;
+      kc = 3 * (fs & 3) + t % 3;
+    }
+    sh.varblk[t] = (unsigned char)kb;
+    sh.varcol[t] = (unsigned char)kc;
+    if (t <= N) {
+      const int b0 = 4 * t, b1 = 4 * t - 64;
+      const unsigned long long lo = (b0 >= 64) ? msk0 : (msk0 & ((1ull << b0) - 1ull));
+      const unsigned long long hi = (b1 <= 0) ? 0ull : (msk1 & ((1ull << b1) - 1ull));
+      sh.blkbase[t] = 3 * (__popcll(lo) + __popcll(hi));
+    }
+    for (int i = t; i < 6 * nfs; i += G::NT) sh.cflag[i] = 0;
+  }
+  Model md;
+  make_model(srec, P.dt, md);
+  make_bdt<G::NT>(srec, md, t, sh.BdtT);
+  wbar();
+  if (t < N) {
+    float e[13];
+    state_error(srec, md, t, srec + CMPC_REC_HDR + 12 * t, e);
+#pragma unroll
+    for (int j = 0; j < 13; j++) sh.P[W_OFF_E + 16 * t + j] = e[j];
+  }
+  wbar();
+  float wts[13];
+#pragma unroll
+  for (int j = 0; j < 12; j++) wts[j] = P.wts[j];
+  wts[12] = 0.f;
+  // gradient recursion ze_i = S e_i + Adt' ze_{i+1} (uniform; thread j < 13 stores component j)
+  {
+    float ze[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) ze[j] = 0.f;
+    for (int i = N - 1; i >= 0; i--) {
+      float e[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) e[j] = sh.P[W_OFF_E + 16 * i + j];
+      recur(md, wts, e, ze);
+      float mine = 0.f;
+#pragma unroll
+      for (int j = 0; j < 13; j++) mine = (t == j) ? ze[j] : mine;
+      if (t < 13) sh.P[W_OFF_ZE + 16 * i + t] = mine;
+    }
+  }
+  wbar();
+
+  // ---- condensation: row r's lanes build H[r][w], w >= r (half h takes every other w of a
+  // block), into packed upper rows of P; both compute the gradient g_r
+  const bool real = r < n;
+  const int rr = (r < NV) ? r : 0;
+  float gv;
+  {
+    const int kv = real ? sh.varblk[r] : 0;
+    const int cv = real ? sh.varcol[r] : 0;
+    float b[13], u1[13], u2[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) b[j] = real ? sh.BdtT[cv][j] : 0.f;
+    n1_mul(md, b, u1);
+    n1_mul(md, u1, u2);
+    {
+      float zk[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) zk[j] = sh.P[W_OFF_ZE + 16 * kv + j];
+      gv = real ? 2.f * dot13(b, zk) : 0.f;  // qg = 2 B_qp' S (A_qp x0 + Q_qp f - X_d)
+    }
+    wbar();  // every ZE read is done before P is overwritten
+    const int myrow = G::prow0(rr);
+    float z[13];
+#pragma unroll
+    for (int j = 0; j < 13; j++) z[j] = 0.f;
+    for (int i = N - 1; i >= 0; i--) {
+      // z_i = S Adt^{i-kv} b_r + Adt' z_{i+1}  (the S term only for i >= kv)
+      const bool act = real && (i >= kv);
+      const float k = (float)(i - kv);
+      const float k2 = 0.5f * k * (k - 1.f);
+      float gk[13];
+#pragma unroll
+      for (int j = 0; j < 13; j++) gk[j] = act ? fmaf(k2, u2[j], fmaf(k, u1[j], b[j])) : 0.f;
+      recur(md, wts, gk, z);
+      const int wb = __builtin_amdgcn_readfirstlane(sh.blkbase[i]);
+      const int we = __builtin_amdgcn_readfirstlane(sh.blkbase[i + 1]);
+      for (int w0 = wb; w0 < we; w0 += 2) {
+        const int w = w0 + h;
+        const int cw = sh.varcol[w];
+        float bw[13];
+#pragma unroll
+        for (int j = 0; j < 13; j++) bw[j] = sh.BdtT[cw][j];
+        float val = 2.f * dot13(bw, z);
+        if (w == r) val += P.alpha2;  // qH = 2 (B'SB + alpha I), SolverMPC.cpp:806
+        if (act && w < we && w >= r) sh.P[myrow + w] = val;
+      }
+    }
+  }
+  wbar();
+
+  // ---- my half-row of H into registers: columns c = 2 j + h (identity padding)
+  float slot[NH];
+  float gb = gv;  // border: g_r, then y_r (both halves keep it)
+  {
+    const int myrow = G::prow0(rr);
+    static_for<0, NH>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      const int c = 2 * j + h;
+      const int addr = (c >= rr) ? myrow + c : G::prow0(c) + rr;
+      const float x = sh.P[addr];
+      slot[j] = (real && c < n) ? x : ((c == r) ? 1.f : 0.f);
+      if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  wbar();
+
+  // ---- bordered Cholesky [H | g]: pivot column k = register k/2 of half k%2 of every row,
+  // published into P's row k (even / odd segments), one s_barrier per step
+  int status = CMPC_OK;
+  float my_inv = 1.f;
+  static_for<0, NV>([&](auto KC) {
+    constexpr int k = decltype(KC)::value;
+    constexpr int kj = k >> 1, kh = k & 1;
+    constexpr int j0 = G::j0(k);
+    constexpr int base = G::fbase(k);
+    constexpr int st = G::seg(k);
+    if (k < n) {
+      const float mine = slot[kj];
+      const float other = pair_other(mine, h);
+      const float hrk = (h == kh) ? mine : other;          // H[r][k] of the trailing matrix
+      if (h == kh && r >= 2 * j0 && r < NV)
+        sh.P[base + (r & 1) * st + (r >> 1) - j0] = (r >= k) ? mine : 0.f;
+      if (r == k && h == 0) sh.gbuf[k] = gb;
+      wbar();
+      float d = sh.P[base + kh * st + kj - j0];
+      if (!(d > 0.f)) { status = CMPC_NOT_PD; d = 1e-30f; }
+      const float inv = rsqrtf(d);
+      if (r == k) { my_inv = inv; if (h == 0) sh.ibuf[k] = inv; }
+      const float a = (r > k && r < NV) ? -hrk * (inv * inv) : 0.f;
+      const float* prow = &sh.P[base + h * st - j0];
+#pragma unroll
+      for (int j = j0; j < NH; j += 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(prow + j);
+        axpy4(a, r4, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+        CMPC_WSWEEP_FENCE(j);
+      }
+      gb = fmaf(a, sh.gbuf[k], gb);
+      wpin(slot);
+    }
+  });
+  const float yv = real ? gb * my_inv : 0.f;  // L y = g
+  if (h == 0 && r < NV) sh.ybuf[r & 1][r >> 1] = yv;
+  wbar();
+
+  // ---- J = L^-T: row r solves L x = e_r over its half of the columns (LDS reads only; the
+  // pivot value x_k lives in the half holding column k: one partner exchange per step)
+  static_for<0, NH>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    slot[j] = (2 * j + h == r) ? 1.f : 0.f;
+  });
+  static_for<0, NV>([&](auto KC) {
+    constexpr int k = decltype(KC)::value;
+    constexpr int kj = k >> 1, kh = k & 1;
+    constexpr int j0 = G::j0(k);
+    constexpr int base = G::fbase(k);
+    constexpr int st = G::seg(k);
+    if (k < n) {
+      wlsync();
+      const float inv = sh.ibuf[k];
+      const float mine = slot[kj];
+      const float other = pair_other(mine, h);
+      const float xk = ((h == kh) ? mine : other) * inv;
+      const float a = -xk * inv;
+      const float* prow = &sh.P[base + h * st - j0];
+#pragma unroll
+      for (int j = j0; j < NH; j += 4) {
+        const float4 r4 = *reinterpret_cast<const float4*>(prow + j);
+        axpy4(a, r4, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+        CMPC_WSWEEP_FENCE(j);
+      }
+      if (h == kh) slot[kj] = xk;
+      wpin(slot);
+    }
+  });
+
+  // ---- unconstrained minimiser x = -J y
+  float xv;
+  {
+    f2v xacc = {0.f, 0.f};
+    const float* yb = &sh.ybuf[h][0];
+#pragma unroll
+    for (int j = 0; j < NH; j += 4) {
+      const float4 y4 = *reinterpret_cast<const float4*>(yb + j);
+      dot4(xacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], y4);
+      CMPC_WSWEEP_FENCE(j);
+    }
+    const float xs2 = pair_sum(xacc.x + xacc.y);
+    xv = real ? -xs2 : 0.f;
+  }
+  wbar();  // the factor rows in P are dead from here; P holds R
+
+  // ---- Goldfarb-Idnani dual active set on the friction pyramids, J's columns relabelled
+  // l = h NH + j. One flat loop, one active-set step per trip; R in P, maintained by wave 0
+  const float mui = P.mu_inv;
+  const float fnorm = rsqrtf(mui * mui + 1.f);
+  int q = 0;
+  int iters = 0;
+  float u_a[RQ], r_a[RQ];
+  int a_a[RQ];
+#pragma unroll
+  for (int m = 0; m < RQ; m++) { u_a[m] = 0.f; r_a[m] = 0.f; a_a[m] = 0; }
+  int p = -1;
+  Cons cp{};
+  float up = 0.f;
+  if (status == CMPC_OK) {
+    for (;;) {
+      wpin(slot);
+      const int t = tid_opq();
+      const int lane = t & 63;
+      const int h = lane >> 5;
+      const int r = 32 * wave + (lane & 31);
+      if (p < 0) {
+        if (h == 0 && r < NV) sh.xs[r] = xv;
+        wbar();
+        // most violated constraint (normalised slack); every wave scans the same foot-steps
+        float best = 0.f, xm = 0.f;
+        int bid = kNoneW;
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+          const int s = lane + 64 * m;
+          if (s < nfs) {
+            const float fx = sh.xs[3 * s], fy = sh.xs[3 * s + 1], fz = sh.xs[3 * s + 2];
+            xm = fmaxf(xm, fmaxf(fabsf(fx), fmaxf(fabsf(fy), fabsf(fz))));
+            float sl[6];
+            sl[0] = (mui * fx + fz) * fnorm;
+            sl[1] = (-mui * fx + fz) * fnorm;
+            sl[2] = (mui * fy + fz) * fnorm;
+            sl[3] = (-mui * fy + fz) * fnorm;
+            sl[4] = fz;
+            sl[5] = sh.sub[s] - fz;
+#pragma unroll
+            for (int u = 0; u < 6; u++)
+              if (!sh.cflag[6 * s + u] && sl[u] < best) { best = sl[u]; bid = 6 * s + u; }
+          }
+        }
+        const float xmax = wave_max(xm);
+        wave_argmin(best, bid);
+        const float tol = 1e-5f * fmaxf(1.f, xmax);
+        if (bid == kNoneW || best >= -tol) break;
+        p = __builtin_amdgcn_readfirstlane(bid);
+        cp = decode_cons(p, mui, sh.sub[p / 6]);
+        up = 0.f;
+      }
+      if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
+      // d = J' n+ : rows ia, iz of J through LDS (logical order)
+      if (r == cp.ia && cp.ia != cp.iz) {
+#pragma unroll
+        for (int j = 0; j < NH; j++) sh.bufA[h * G::HOFF + j] = slot[j];
+      }
+      if (r == cp.iz) {
+#pragma unroll
+        for (int j = 0; j < NH; j++) sh.bufB[h * G::HOFF + j] = slot[j];
+      }
+      if (h == 0 && r < NV) sh.xs[r] = xv;
+      wbar();
+      // thread t < NV: logical column t
+      float dv = 0.f, dm = 0.f;
+      if (t < NV) {
+        const int li = lidx<NV>(t);
+        dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[li], cp.cb * sh.bufB[li]) : cp.cb * sh.bufB[li];
+        dm = (t >= q) ? dv : 0.f;
+        sh.vbuf[li] = dm;
+        sh.dfull[t] = dv;
+      }
+      {
+        const float dw = wave_sum(dv * dv);
+        if (lane == 0) sh.redf[wave] = dw;
+      }
+      const float spv = fmaf(cp.ca, sh.xs[cp.ia], fmaf(cp.cb, sh.xs[cp.iz], -cp.bp));
+      wbar();
+      // z_r = J_r . dm (primal step direction), zn = |dm|^2 = z' n+, dn = |d|^2
+      float zv, zn, dn = 0.f;
+      {
+        f2v zacc = {0.f, 0.f}, nacc = {0.f, 0.f};
+        const float* vb = &sh.vbuf[h * G::HOFF];
+#pragma unroll
+        for (int j = 0; j < NH; j += 4) {
+          const float4 m4 = *reinterpret_cast<const float4*>(vb + j);
+          dot4(zacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], m4);
+          dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
+          CMPC_WSWEEP_FENCE(j);
+        }
+        zv = pair_sum(zacc.x + zacc.y);
+        zn = pair_sum(nacc.x + nacc.y);
+#pragma unroll
+        for (int w = 0; w < G::NW; w++) dn += sh.redf[w];
+      }
+      // r = R^-1 d1 by back substitution (wave 0), then the dual step t1 = min u_j / r_j
+      if (wave == 0) {
+        float acc[RQ];
+#pragma unroll
+        for (int m = 0; m < RQ; m++) {
+          acc[m] = (lane + 64 * m < NV) ? sh.dfull[(lane + 64 * m) < NV ? lane + 64 * m : 0] : 0.f;
+          r_a[m] = 0.f;
+        }
+        for (int i = q - 1; i >= 0; i--) {
+          const int off = rcol_w(i);
+          const float ri = wdiv(rl_pos<RQ>(acc, i), sh.P[off + i]);
+#pragma unroll
+          for (int m = 0; m < RQ; m++) {
+            const int pos = lane + 64 * m;
+            if (pos < i) acc[m] = fmaf(-sh.P[off + pos], ri, acc[m]);
+            r_a[m] = (pos == i) ? ri : r_a[m];
+          }
+        }
+        float t1w = kBigF;
+        int kw = kNoneW;
+#pragma unroll
+        for (int m = 0; m < RQ; m++) {
+          const int pos = lane + 64 * m;
+          if (pos < q && r_a[m] > 0.f) {
+            const float th = fmaxf(wdiv(u_a[m], r_a[m]), 0.f);
+            if (th < t1w) { t1w = th; kw = pos; }
+          }
+        }
+        wave_argmin(t1w, kw);
+        if (lane == 0) { sh.redf[8] = t1w; sh.redi[8] = kw; }
+      }
+      wbar();
+      const float t1 = sh.redf[8];
+      const int kk = __builtin_amdgcn_readfirstlane(sh.redi[8]);
+      const bool zero_step = !(zn > 1e-9f * dn);
+      const float t2 = zero_step ? kBigF : -wdiv(spv, zn);
+      const float tt = fminf(t1, t2);
+      if (tt >= kBigF) { status = CMPC_INFEASIBLE; break; }
+      if (wave == 0) {
+#pragma unroll
+        for (int m = 0; m < RQ; m++)
+          if (lane + 64 * m < q) u_a[m] = fmaf(-tt, r_a[m], u_a[m]);
+      }
+      up += tt;
+      if (!zero_step) xv = fmaf(tt, zv, xv);
+      const bool add = !zero_step && t2 <= t1;
+      float beta = 0.f;
+      bool seam = false;   // a drop whose Givens chain crosses into half 1
+      if (add) {
+        // ---- add p: Householder reflection on logical columns q.., R gains column (d1, -sgn ts)
+        const float ts = sqrtf(zn);
+        const float dq = sh.dfull[q];
+        const float sgn = (dq >= 0.f) ? 1.f : -1.f;
+        beta = fast_rcp(ts * (ts + fabsf(dq)));  // 2 / (w'w)
+        if (t < NV) {
+          sh.vbuf[lidx<NV>(t)] = (t == q) ? dq + sgn * ts : dm;
+          *reinterpret_cast<float2*>(&sh.cs[2 * t + (t >= NH ? 4 : 0)]) = make_float2(1.f, 0.f);
+          const int offq = rcol_w(q);
+          if (t < q) sh.P[offq + t] = dv;
+          if (t == q) sh.P[offq + q] = -sgn * ts;
+        }
+        if (wave == 0) {
+#pragma unroll
+          for (int m = 0; m < RQ; m++)
+            if (lane + 64 * m == q) { u_a[m] = up; a_a[m] = p; }
+        }
+        if (t == 0) sh.cflag[p] = 1;
+      } else {
+        // ---- drop active constraint kk: shift positions kk+1..q-1 down, remove column kk of R,
+        // re-triangularise rows kk..q-1 with Givens rotations (wave 0, in place)
+        const int k = kk;
+        seam = (q > NH);
+        if (t < NV) {
+          sh.vbuf[lidx<NV>(t)] = 0.f;
+          if (t < k || t > q - 2)
+            *reinterpret_cast<float2*>(&sh.cs[2 * t + (t >= NH ? 4 : 0)]) = make_float2(1.f, 0.f);
+        }
+        if (wave == 0) {
+          const int ak = rli_pos<RQ>(a_a, k);
+          if (lane == 0) sh.cflag[ak] = 0;
+          // position j <- j + 1 for k <= j < q - 1
+          int a_nx[RQ];
+          float u_nx[RQ];
+#pragma unroll
+          for (int m = 0; m < RQ; m++) {
+            a_nx[m] = lane_next_i(a_a[m], a_a[m]);
+            u_nx[m] = lane_next(u_a[m], u_a[m]);
+            if (m + 1 < RQ) {
+              const int a0 = rli(a_a[m + 1 < RQ ? m + 1 : m], 0);
+              const float u0 = rl(u_a[m + 1 < RQ ? m + 1 : m], 0);
+              if (lane == 63) { a_nx[m] = a0; u_nx[m] = u0; }
+            }
+          }
+#pragma unroll
+          for (int m = 0; m < RQ; m++) {
+            const int pos = lane + 64 * m;
+            if (pos >= k && pos < q - 1) { a_a[m] = a_nx[m]; u_a[m] = u_nx[m]; }
+          }
+          // new column c (k <= c <= q-2) = old column c+1; lane handles c = lane + 64 m. Every
+          // read of an old entry precedes, in this wavefront's LDS order, the write reusing it
+          float top[RQ];
+          bool in_c[RQ];
+#pragma unroll
+          for (int m = 0; m < RQ; m++) {
+            const int c = lane + 64 * m;
+            in_c[m] = c >= k && c <= q - 2;
+            top[m] = in_c[m] ? sh.P[rcol_w(c + 1) + k] : 0.f;
+          }
+          wlsync();
+          for (int rw = 0; rw < k; rw++) {
+            float xr[RQ];
+#pragma unroll
+            for (int m = 0; m < RQ; m++) {
+              const int c = lane + 64 * m;
+              xr[m] = in_c[m] ? sh.P[rcol_w(c + 1) + rw] : 0.f;
+            }
+            wlsync();
+#pragma unroll
+            for (int m = 0; m < RQ; m++) {
+              const int c = lane + 64 * m;
+              if (in_c[m]) sh.P[rcol_w(c) + rw] = xr[m];
+            }
+            wlsync();
+          }
+          for (int j = k; j <= q - 2; j++) {
+            float bot[RQ];
+#pragma unroll
+            for (int m = 0; m < RQ; m++) {
+              const int c = lane + 64 * m;
+              bot[m] = (in_c[m] && c >= j) ? sh.P[rcol_w(c + 1) + j + 1] : 0.f;
+            }
+            wlsync();
+            const float a0 = rl_pos<RQ>(top, j), b0 = rl_pos<RQ>(bot, j);
+            const float hh = sqrtf(a0 * a0 + b0 * b0);
+            float cc = 1.f, sn = 0.f;
+            if (hh > 0.f) { const float ih = fast_rcp(hh); cc = a0 * ih; sn = b0 * ih; }
+#pragma unroll
+            for (int m = 0; m < RQ; m++) {
+              const int c = lane + 64 * m;
+              if (in_c[m] && c >= j) {
+                sh.P[rcol_w(c) + j] = fmaf(cc, top[m], sn * bot[m]);
+                top[m] = fmaf(-sn, top[m], cc * bot[m]);
+              }
+            }
+            if (lane == 0)
+              *reinterpret_cast<float2*>(&sh.cs[2 * j + (j >= NH ? 4 : 0)]) = make_float2(cc, sn);
+            wlsync();
+          }
+        }
+      }
+      wbar();
+      // J <- J (I - beta w w'): tw = J_r . w over both halves, J_r -= beta tw w (no-op on a drop)
+      {
+        f2v tacc = {0.f, 0.f};
+        const float* vb = &sh.vbuf[h * G::HOFF];
+#pragma unroll
+        for (int j = 0; j < NH; j += 4) {
+          const float4 w4 = *reinterpret_cast<const float4*>(vb + j);
+          dot4(tacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], w4);
+          CMPC_WSWEEP_FENCE(j);
+        }
+        const float bt = -beta * pair_sum(tacc.x + tacc.y);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < NH; j += 4) {
+          const float4 w4 = *reinterpret_cast<const float4*>(vb + j);
+          axpy4(bt, w4, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+          CMPC_WSWEEP_FENCE(j);
+        }
+      }
+      // J columns (l, l+1) <- Givens chain, ascending l (identity on an add)
+      const float* csb = &sh.cs[h * (2 * NH + 4)];
+      if (!seam) {
+        // every rotation lies in half 0 (active set <= NV/2); half 1 reads identities
+        static_for<0, NH - 1>([&](auto JC) {
+          constexpr int j = decltype(JC)::value;
+          const float2 c2 = *reinterpret_cast<const float2*>(csb + 2 * j);
+          const float x0 = slot[j], x1 = slot[j + 1];
+          slot[j] = fmaf(c2.x, x0, c2.y * x1);
+          slot[j + 1] = fmaf(-c2.y, x0, c2.x * x1);
+          if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        });
+      } else {
+        // half 0's chain, the seam rotation (logical NH-1, NH), then half 1's chain
+        static_for<0, NH - 1>([&](auto JC) {
+          constexpr int j = decltype(JC)::value;
+          float2 c2 = *reinterpret_cast<const float2*>(csb + 2 * j);
+          if (h) c2 = make_float2(1.f, 0.f);
+          const float x0 = slot[j], x1 = slot[j + 1];
+          slot[j] = fmaf(c2.x, x0, c2.y * x1);
+          slot[j + 1] = fmaf(-c2.y, x0, c2.x * x1);
+          if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        });
+        {
+          const float2 c2 = *reinterpret_cast<const float2*>(&sh.cs[2 * (NH - 1)]);
+          const float mine = h ? slot[0] : slot[NH - 1];
+          const float other = pair_other(mine, h);
+          if (h == 0) slot[NH - 1] = fmaf(c2.x, mine, c2.y * other);
+          else slot[0] = fmaf(-c2.y, other, c2.x * mine);
+        }
+        static_for<0, NH - 1>([&](auto JC) {
+          constexpr int j = decltype(JC)::value;
+          float2 c2 = *reinterpret_cast<const float2*>(csb + 2 * j);
+          if (!h) c2 = make_float2(1.f, 0.f);
+          const float x0 = slot[j], x1 = slot[j + 1];
+          slot[j] = fmaf(c2.x, x0, c2.y * x1);
+          slot[j + 1] = fmaf(-c2.y, x0, c2.x * x1);
+          if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        });
+      }
+      if (add) {
+        q++;
+        p = -1;
+      } else {
+        q--;
+      }
+    }
+  }
+
+  // ---- scatter (q_soln layout 12 k + 3 leg + axis, swing -> 0) staged in LDS, coalesced out
+  const bool ok = (status == CMPC_OK);
+  wbar();
+  for (int i = t; i < 12 * N; i += G::NT) sh.P[i] = 0.f;
+  wbar();
+  if (ok && h == 0 && real) sh.P[12 * sh.varblk[r] + sh.varcol[r]] = xv;
+  wbar();
+  for (int i = 4 * t; i < 12 * N; i += 4 * G::NT)
+    *reinterpret_cast<float4*>(&fout[i]) = *reinterpret_cast<const float4*>(&sh.P[i]);
+  if (t == 0) {
+    st_out[0] = (uint8_t)status;
+    if (it_out) it_out[0] = iters;
+  }
+}
+
+}  // namespace
+
+// One workgroup per entry of the class's list; the grid is sized for the worst case (the list
+// length is only known on the device) and surplus workgroups exit at once.
+#if CMPC_WIDE_VGPR_CAP > 0
+#define CMPC_WIDE_VGPR_ATTR __attribute__((amdgpu_num_vgpr(CMPC_WIDE_VGPR_CAP)))
+#else
+#define CMPC_WIDE_VGPR_ATTR
+#endif
+template <int NV>
+__global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGPR_ATTR void cmpc_solve_w_kernel(
+    const float* __restrict__ recs, KParams P, float* __restrict__ forces,
+    uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
+    const int* __restrict__ in_count) {
+  __shared__ SharedW<NV> sh;
+  const int b = blockIdx.x;
+  if (b >= *in_count) return;
+  const int inst = in_list[b];
+  solve_w<NV>(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
+              status + inst, iters ? iters + inst : nullptr);
+}
+
+template <int NV>
+hipError_t launch_wide_impl(const float* d_recs, const KParams& P, float* d_forces,
+                            uint8_t* d_status, int32_t* d_iters, const int* in_list,
+                            const int* in_count, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(cmpc_solve_w_kernel<NV>, dim3(grid), dim3(WGeo<NV>::NT), 0, stream, d_recs, P,
+                     d_forces, d_status, d_iters, in_list, in_count);
+  return hipGetLastError();
+}
+
+}  // namespace cmpc

@@ -8,7 +8,8 @@ nominal stance, a trot contact table at a random phase (``Gait.cpp:159-188``,
 ``updateMPCIfNeeded`` does (``ConvexMPCLocomotion.cpp:554-585``). A fraction of instances get
 Bernoulli(0.5) contacts instead (stress / ragged reduced sizes).
 
-Deterministic: numpy ``Generator(Philox(seed))``, fully vectorised.
+Deterministic and shard-reproducible: one Philox4x32-10 stream per instance id, fully
+vectorised.
 """
 from __future__ import annotations
 
@@ -49,44 +50,123 @@ def euler_zyx_to_quat(roll, pitch, yaw):
     return np.stack([w, x, y, z], axis=-1)
 
 
+# ---------------------------------------------------------------------------------------------
+# Per-instance counter-based randomness: instance ``id`` draws from
+# Philox4x32-10 with key (base seed, 0x5EED0000 + id) and counters 0, 1, 2, ... Any contiguous
+# shard [first_id, first_id + batch) therefore reproduces exactly the instances a 1-GPU run
+# generates for those ids, whatever the world size.
+# ---------------------------------------------------------------------------------------------
+_PHILOX_M0, _PHILOX_M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_PHILOX_W0, _PHILOX_W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
+_MASK32 = np.uint64(0xFFFFFFFF)
+SEED_TAG = 0x5EED0000
+
+
+def philox4x32(key0: np.ndarray, key1: np.ndarray, blocks: int) -> np.ndarray:
+    """Philox4x32-10 (Salmon et al., SC'11) over counters (c, 0, 0, 0), c < ``blocks``, one key
+    per row: returns uint32 [len(key0), 4 * blocks]."""
+    k0 = np.broadcast_to(np.asarray(key0, np.uint64)[:, None], (len(key0), blocks)).copy()
+    k1 = np.broadcast_to(np.asarray(key1, np.uint64)[:, None], (len(key0), blocks)).copy()
+    c0 = np.broadcast_to(np.arange(blocks, dtype=np.uint64)[None, :], k0.shape).copy()
+    c1 = np.zeros_like(c0)
+    c2 = np.zeros_like(c0)
+    c3 = np.zeros_like(c0)
+    for r in range(10):
+        p0 = _PHILOX_M0 * c0
+        p1 = _PHILOX_M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & _MASK32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & _MASK32
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        if r < 9:
+            k0 = (k0 + _PHILOX_W0) & _MASK32
+            k1 = (k1 + _PHILOX_W1) & _MASK32
+    out = np.stack([c0, c1, c2, c3], axis=-1).astype(np.uint32)
+    return out.reshape(len(key0), 4 * blocks)
+
+
+# fixed draw slots per instance (uniforms in (0, 1); a normal takes two slots, Box-Muller)
+_S_ROLL, _S_PITCH, _S_YAW, _S_PX, _S_PY, _S_PZ = 0, 2, 4, 5, 6, 8
+_S_VX, _S_VY, _S_VZ, _S_W, _S_BX, _S_BY, _S_RZ = 10, 11, 12, 14, 20, 28, 36
+_S_PHASE, _S_RND, _S_VDX, _S_VDY, _S_YAWRATE, _S_XS, _S_YS, _S_YAWN, _S_XDRAG = (
+    44, 45, 46, 47, 48, 49, 50, 51, 53)
+_S_FIXED = 64          # then 4N Bernoulli slots of the random contact tables
+
+
+class _Draws:
+    def __init__(self, u32: np.ndarray):
+        self.u = (u32.astype(np.float64) + 0.5) * (1.0 / 4294967296.0)
+
+    def uniform(self, slot, lo=0.0, hi=1.0, count=1):
+        x = self.u[:, slot:slot + count]
+        x = lo + (hi - lo) * x
+        return x[:, 0] if count == 1 else x
+
+    def normal(self, slot, mu=0.0, sd=1.0, count=1):
+        u1 = self.u[:, slot:slot + 2 * count:2]
+        u2 = self.u[:, slot + 1:slot + 2 * count:2]
+        z = np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+        x = mu + sd * z
+        return x[:, 0] if count == 1 else x
+
+
+def instance_draws(first_id: int, batch: int, horizon: int, seed: int = BASE_SEED) -> _Draws:
+    ids = np.arange(first_id, first_id + batch, dtype=np.uint64)
+    key0 = np.full(batch, seed & 0xFFFFFFFF, np.uint64)
+    key1 = (ids + np.uint64(SEED_TAG)) & _MASK32
+    blocks = (_S_FIXED + 4 * horizon + 3) // 4
+    return _Draws(philox4x32(key0, key1, blocks))
+
+
 def make_instances(batch: int, horizon: int = 10, seed: int = BASE_SEED, dt: float = 0.026,
                    random_contact_frac: float = 0.25, body_height: float = 0.29,
-                   x_drag_range: float = 0.5, stress: bool = False) -> np.ndarray:
-    """Return packed records [batch, record_words(horizon)] (float32).
+                   x_drag_range: float = 0.5, stress: bool = False, first_id: int = 0,
+                   chunk: int = 65536) -> np.ndarray:
+    """Return packed records [batch, record_words(horizon)] (float32) for instance ids
+    ``first_id .. first_id + batch - 1``.
 
-    ``stress`` widens the velocity/orientation errors so friction cones bind (active sets)."""
-    g = np.random.Generator(np.random.Philox(seed))
+    Every instance draws from its own Philox stream (key = (seed, 0x5EED0000 + id)), so a shard
+    of ids reproduces the same instances as a whole-batch call. ``stress`` widens the
+    velocity/orientation errors so friction cones bind (active sets)."""
+    if batch > chunk:  # bounded temporaries for very large batches
+        return np.concatenate([
+            make_instances(min(chunk, batch - a), horizon, seed, dt, random_contact_frac,
+                           body_height, x_drag_range, stress, first_id + a, chunk)
+            for a in range(0, batch, chunk)], axis=0)
     B, N = batch, horizon
+    d = instance_draws(first_id, B, N, seed)
     scale = 3.0 if stress else 1.0
-    roll = np.clip(g.normal(0, 0.05 * scale, B), -0.3 * scale, 0.3 * scale)
-    pitch = np.clip(g.normal(0, 0.05 * scale, B), -0.3 * scale, 0.3 * scale)
-    yaw = g.uniform(-np.pi, np.pi, B)
+    roll = np.clip(d.normal(_S_ROLL, 0, 0.05 * scale), -0.3 * scale, 0.3 * scale)
+    pitch = np.clip(d.normal(_S_PITCH, 0, 0.05 * scale), -0.3 * scale, 0.3 * scale)
+    yaw = d.uniform(_S_YAW, -np.pi, np.pi)
     q = euler_zyx_to_quat(roll, pitch, yaw)
-    p = np.stack([g.uniform(-1, 1, B), g.uniform(-1, 1, B), body_height + g.normal(0, 0.02, B)], -1)
-    v = np.stack([g.uniform(-0.7, 0.7, B) * scale, g.uniform(-0.4, 0.4, B) * scale,
-                  g.normal(0, 0.05, B)], -1)
-    w = g.normal(0, 0.3 * scale, (B, 3))
+    p = np.stack([d.uniform(_S_PX, -1, 1), d.uniform(_S_PY, -1, 1),
+                  body_height + d.normal(_S_PZ, 0, 0.02)], -1)
+    v = np.stack([d.uniform(_S_VX, -0.7, 0.7) * scale, d.uniform(_S_VY, -0.4, 0.4) * scale,
+                  d.normal(_S_VZ, 0, 0.05)], -1)
+    w = d.normal(_S_W, 0, 0.3 * scale, count=3)
     # foot offsets r = pFoot - p in world frame (axis-major, ConvexMPCLocomotion.cpp:786-790)
     cy, sy = np.cos(yaw)[:, None], np.sin(yaw)[:, None]
-    bx = _HIP_X[None, :] + g.normal(0, 0.03, (B, 4))
-    by = _HIP_Y[None, :] + g.normal(0, 0.03, (B, 4))
+    bx = _HIP_X[None, :] + d.normal(_S_BX, 0, 0.03, count=4)
+    by = _HIP_Y[None, :] + d.normal(_S_BY, 0, 0.03, count=4)
     rx = cy * bx - sy * by
     ry = sy * bx + cy * by
-    rz = -p[:, 2:3] + g.normal(0, 0.02, (B, 4))
+    rz = -p[:, 2:3] + d.normal(_S_RZ, 0, 0.02, count=4)
     r = np.concatenate([rx, ry, rz], axis=1)
     # contact table: trot at a random phase; a fraction with Bernoulli(0.5) contacts
-    gait = trot_table(N, g.integers(0, 18, B))
-    rnd = g.random(B) < random_contact_frac
+    phase = np.minimum((d.uniform(_S_PHASE) * 18).astype(np.int64), 17)
+    gait = trot_table(N, phase)
+    rnd = d.uniform(_S_RND) < random_contact_frac
     if rnd.any():
-        gait[rnd] = (g.random((int(rnd.sum()), 4 * N)) < 0.5).astype(np.int32)
+        bern = d.uniform(_S_FIXED, count=4 * N).reshape(B, 4 * N)
+        gait[rnd] = (bern[rnd] < 0.5).astype(np.int32)
     # trajectory (ConvexMPCLocomotion.cpp:554-585)
-    vdes_x = g.uniform(-0.7, 0.7, B) * scale
-    vdes_y = g.uniform(-0.4, 0.4, B) * scale
-    yaw_rate = g.uniform(-2.5, 2.5, B)
-    x_start = p[:, 0] + g.uniform(-0.1, 0.1, B)
-    y_start = p[:, 1] + g.uniform(-0.1, 0.1, B)
+    vdes_x = d.uniform(_S_VDX, -0.7, 0.7) * scale
+    vdes_y = d.uniform(_S_VDY, -0.4, 0.4) * scale
+    yaw_rate = d.uniform(_S_YAWRATE, -2.5, 2.5)
+    x_start = p[:, 0] + d.uniform(_S_XS, -0.1, 0.1)
+    y_start = p[:, 1] + d.uniform(_S_YS, -0.1, 0.1)
     traj = np.zeros((B, N, 12), np.float32)
-    traj[:, :, 2] = (yaw + g.normal(0, 0.05, B))[:, None]   # _yaw_des
+    traj[:, :, 2] = (yaw + d.normal(_S_YAWN, 0, 0.05))[:, None]   # _yaw_des
     traj[:, :, 3] = x_start[:, None]
     traj[:, :, 4] = y_start[:, None]
     traj[:, :, 5] = body_height
@@ -98,7 +178,7 @@ def make_instances(batch: int, horizon: int = 10, seed: int = BASE_SEED, dt: flo
         traj[:, i, 3] = traj[:, i - 1, 3] + np.float32(dt) * traj[:, i, 9]
         traj[:, i, 4] = traj[:, i - 1, 4] + np.float32(dt) * traj[:, i, 10]
         traj[:, i, 2] = traj[:, i - 1, 2] + np.float32(dt) * traj[:, i, 8]
-    x_drag = g.uniform(-x_drag_range, x_drag_range, B)
+    x_drag = d.uniform(_S_XDRAG, -x_drag_range, x_drag_range)
     rpy = np.stack([roll, pitch, yaw], -1)
     return pack_records(p, v, q, w, r, traj.reshape(B, 12 * N), gait, rpy=rpy, x_drag=x_drag)
 

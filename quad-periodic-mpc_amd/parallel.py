@@ -41,6 +41,8 @@ def shard_sizes(batch: int, world: int) -> list[int]:
 
 
 def _group_info(group):
+    if not dist.is_available() or not dist.is_initialized():
+        return 1, 0          # single process: no collectives
     return dist.get_world_size(group), dist.get_rank(group)
 
 
@@ -143,6 +145,186 @@ class ShardedSolver:
                                 group=self.group, device=self.device)
         forces, status = self.solve_local(local)
         return gather_forces(forces, self.global_batch, dst=src, group=self.group), status
+
+    def close(self):
+        if self._solver is not None:
+            self._solver.close()
+            self._solver = None
+
+
+def _chunk_plan(batch: int, world: int, chunks: int):
+    """Per rank r and chunk c: rows [a_rc, b_rc) of the global batch (contiguous rank shards,
+    each split into ``chunks`` contiguous pieces) and S_c = the largest piece c over ranks (the
+    collective size; shorter pieces are padded)."""
+    plan = []
+    for r in range(world):
+        a, b = shard_bounds(batch, world, r)
+        plan.append([(a + lo, a + hi) for lo, hi in
+                     (shard_bounds(b - a, chunks, c) for c in range(chunks))])
+    sizes = [max(plan[r][c][1] - plan[r][c][0] for r in range(world)) for c in range(chunks)]
+    return plan, sizes
+
+
+class RootPipeline:
+    """BASELINE config 4 / SURVEY.md §8(e): the records of the whole batch live on root ``src``;
+    one :meth:`step` scatters them over the ranks (RCCL over xGMI under the ``nccl`` backend),
+    solves every rank's contiguous shard on its own GPU and gathers the forces back to root.
+
+    The shard of every rank is cut into ``chunks`` pieces and the three stages are software-
+    pipelined: the collectives run on the process group's communication stream, the solve on the
+    caller's current stream, so piece c+1 is in flight over xGMI while piece c is being solved
+    and piece c-1 is being gathered. Issue order per step (communication stream):
+    scatter 0, scatter 1, gather 0, scatter 2, gather 1, ... — a gather never delays the next
+    piece's scatter.
+
+    ``solve_fn(records, forces, status)`` solves rows in place (device tensors of this rank);
+    the default binds a :class:`BatchSolver` to the current stream. Every buffer is allocated
+    here, none inside :meth:`step`."""
+
+    def __init__(self, params, global_batch: int, chunks: int = 4, *, group=None, device=None,
+                 src: int = 0, solve_fn=None, record_words: Optional[int] = None):
+        from .records import record_words as _rw
+        self.params = params
+        self.N = params.horizon
+        self.words = record_words or _rw(self.N)
+        self.batch = int(global_batch)
+        self.group = group
+        self.src = src
+        self.world, self.rank = _group_info(group)
+        self.chunks = max(1, min(int(chunks), max(1, self.batch // max(1, self.world))))
+        self.plan, self.sizes = _chunk_plan(self.batch, self.world, self.chunks)
+        self.start, self.stop = shard_bounds(self.batch, self.world, self.rank)
+        self.local_batch = self.stop - self.start
+        self.device = device
+        dev = device
+        cols = 12 * self.N
+        # this rank's rows: records in, forces / status out (chunk c = rows of plan[rank][c])
+        self._last_root = None
+        # at world 1 the records are solved where they lie (no local copy)
+        self.local_recs = torch.zeros((self.local_batch if self.world > 1 else 0, self.words),
+                                      dtype=torch.float32, device=dev)
+        self.local_forces = torch.zeros((self.local_batch, cols), dtype=torch.float32, device=dev)
+        self.local_status = torch.zeros(self.local_batch, dtype=torch.uint8, device=dev)
+        self.forces = (torch.zeros((self.batch, cols), dtype=torch.float32, device=dev)
+                       if self.rank == src else None)
+        # padded staging only where a piece is shorter than its collective size
+        self._recv = {}
+        self._send = {}
+        self._root_send = {}
+        self._root_recv = {}
+        for c in range(self.chunks):
+            S = self.sizes[c]
+            a, b = self._local(c)
+            if b - a < S:
+                self._recv[c] = torch.zeros((S, self.words), dtype=torch.float32, device=dev)
+                self._send[c] = torch.zeros((S, cols), dtype=torch.float32, device=dev)
+            if self.rank == src:
+                for r in range(self.world):
+                    ra, rb = self.plan[r][c]
+                    if rb - ra < S:
+                        self._root_send[(r, c)] = torch.zeros((S, self.words), dtype=torch.float32, device=dev)
+                        self._root_recv[(r, c)] = torch.zeros((S, cols), dtype=torch.float32, device=dev)
+        self._solve_fn = solve_fn
+        self._solver = None
+        if solve_fn is None:
+            import importlib
+            solver_mod = importlib.import_module(__package__ + ".solver")
+            stream = torch.cuda.current_stream(dev)
+            self._solver = solver_mod.BatchSolver(params, max_batch=max(1, max(self.sizes)),
+                                                  stream=stream)
+
+    def _local(self, c):
+        a, b = self.plan[self.rank][c]
+        return a - self.start, b - self.start
+
+    def _solve_piece(self, c):
+        a, b = self._local(c)
+        if b <= a:
+            return
+        if self._solve_fn is not None:
+            self._solve_fn(self.local_recs[a:b], self.local_forces[a:b], self.local_status[a:b])
+        else:
+            self._solver.solve(self.local_recs[a:b], self.local_forces[a:b], self.local_status[a:b])
+
+    def _scatter(self, records_root, c):
+        S = self.sizes[c]
+        a, b = self._local(c)
+        out = self._recv.get(c, self.local_recs[a:a + S])
+        lst = None
+        if self.rank == self.src:
+            lst = []
+            for r in range(self.world):
+                ra, rb = self.plan[r][c]
+                if (r, c) in self._root_send:
+                    buf = self._root_send[(r, c)]
+                    buf[:rb - ra].copy_(records_root[ra:rb])
+                    lst.append(buf)
+                else:
+                    lst.append(records_root[ra:rb])
+        return dist.scatter(out, lst, src=self.src, group=self.group, async_op=True)
+
+    def _gather(self, c):
+        S = self.sizes[c]
+        a, b = self._local(c)
+        if c in self._send:
+            self._send[c][:b - a].copy_(self.local_forces[a:b])
+            send = self._send[c]
+        else:
+            send = self.local_forces[a:a + S]
+        lst = None
+        if self.rank == self.src:
+            lst = []
+            for r in range(self.world):
+                ra, rb = self.plan[r][c]
+                lst.append(self._root_recv[(r, c)] if (r, c) in self._root_recv
+                           else self.forces[ra:rb])
+        return dist.gather(send, lst, dst=self.src, group=self.group, async_op=True)
+
+    def _finish_gather(self, c, work):
+        work.wait()
+        if self.rank == self.src:
+            for r in range(self.world):
+                if (r, c) in self._root_recv:
+                    ra, rb = self.plan[r][c]
+                    self.forces[ra:rb].copy_(self._root_recv[(r, c)][:rb - ra])
+
+    def step(self, records_root: Optional[torch.Tensor]) -> None:
+        """One pass: scatter -> solve -> gather, pipelined over the chunks. On root the forces of
+        the whole batch land in :attr:`forces` (complete once the current stream reaches the
+        point after this call)."""
+        self._last_root = records_root
+        if self.rank == self.src and (records_root is None or
+                                      tuple(records_root.shape) != (self.batch, self.words)):
+            raise ValueError(f"root must pass records of shape ({self.batch}, {self.words})")
+        C = self.chunks
+        if self.world == 1:   # nothing to move: solve the resident records in place
+            for c in range(C):
+                a, b = self.plan[0][c]
+                if b > a:
+                    fn = self._solve_fn or self._solver.solve
+                    fn(records_root[a:b], self.forces[a:b], self.local_status[a:b])
+            return
+        sc = [None] * C
+        ga = [None] * C
+        sc[0] = self._scatter(records_root, 0)
+        for c in range(C):
+            if c + 1 < C:
+                sc[c + 1] = self._scatter(records_root, c + 1)
+            sc[c].wait()
+            if c in self._recv:
+                a, b = self._local(c)
+                self.local_recs[a:b].copy_(self._recv[c][:b - a])
+            self._solve_piece(c)
+            ga[c] = self._gather(c)
+        for c in range(C):
+            self._finish_gather(c, ga[c])
+
+    def solve_only(self) -> None:
+        """The same pieces solved with no collective (kernel-only rate of the shard)."""
+        if self.world == 1:
+            return self.step(self._last_root)
+        for c in range(self.chunks):
+            self._solve_piece(c)
 
     def close(self):
         if self._solver is not None:

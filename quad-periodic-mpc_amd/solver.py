@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
     "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
     "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing", "cmpc_batch_estimate",
-    "cmpc_batch_assemble", "cmpc_batch_rollout",
+    "cmpc_batch_assemble", "cmpc_batch_rollout", "cmpc_batch_admm",
 )
 
 _lib = None
@@ -198,7 +198,13 @@ class BatchSolver:
         h = ctypes.c_void_p()
         s = None
         if stream is not None:
-            s = ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream))
+            handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+            if not handle:
+                # NULL would make the library create a private stream, unordered with the
+                # caller's default-stream work: refuse instead of silently racing
+                raise CmpcError("BatchSolver(stream=...) needs a non-default stream "
+                                "(e.g. torch.cuda.Stream()); pass None for a private stream")
+            s = ctypes.c_void_p(handle)
         _check(self.lib.cmpc_batch_create(ctypes.byref(h), ctypes.byref(self.params),
                                           self.max_batch, s), "cmpc_batch_create")
         self._h = h

@@ -101,15 +101,81 @@ def test_admm_tight_matches_qpoases(cm):
 
 
 @pytest.mark.gpu
-def test_admm_rejects_long_horizon(cm):
+@pytest.mark.parametrize("name,reduced", [("n16_trot", False), ("n12_allstance", True),
+                                          ("n12_allstance", False)])
+def test_admm_global_slab_matches_qpoases(cm, name, reduced):
+    """QPs beyond 120 variables (the full QP at the deployed N = 16, n = 192; the reduced
+    all-stance QP at N = 12, n = 144) keep M^-1 in a global fp64 slab: with tight settings they
+    reach the qpOASES optimum like the LDS path does."""
     solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
     solver_mod.load_library()
-    import torch
-    prm = cm.make_params(16)
-    recs = cm.make_instances(2, 16)
-    with pytest.raises(solver_mod.CmpcError):
-        _run(cm, solver_mod, recs, prm, TIGHT)
-    torch.cuda.synchronize()
+    g = load_golden(name)
+    prm = golden_params(cm, g)
+    _, _, f, status, iters = _run(cm, solver_mod, g["records"], prm, dict(TIGHT, reduced=reduced))
+    assert (status == 0).all(), status
+    err = rel_force_err(f, g["q_ref"])
+    assert err.max() <= 1e-4, (err.max(), int(err.argmax()))
+
+
+@pytest.mark.gpu
+def test_admm_global_slab_matches_oracle_iterates(cm, orc):
+    """Deployed settings on n12_allstance reduced (n = 144, global slab): iterates follow the
+    oracle's runFromDense restatement (same termination iteration -> solutions within 1e-6)."""
+    solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+    solver_mod.load_library()
+    g = load_golden("n12_allstance")
+    prm = golden_params(cm, g)
+    recs = g["records"]
+    settings = dict(max_iter=10000, rho=1e-7, sigma=1e-8, alpha=1.5, terminate=0.1)
+    H, gv, f, status, iters = _run(cm, solver_mod, recs, prm, dict(settings, reduced=True))
+    same = 0
+    for i in range(recs.shape[0]):
+        A, u = orc.fmat_ub(recs[i], prm)
+        kv = _kept(recs[i], prm)
+        kr = np.concatenate([np.arange(5 * (v // 3), 5 * (v // 3) + 5) for v in kv[::3]]).astype(int)
+        x, it, ok = orc.jcqp_admm(H[i][np.ix_(kv, kv)], gv[i][kv], A[np.ix_(kr, kv)], u[kr],
+                                  **settings)
+        full = np.zeros(H.shape[1])
+        full[kv] = x
+        assert status[i] == (0 if ok else 1)
+        if iters[i] == it:
+            same += 1
+            assert rel_force_err(f[i:i + 1], full[None])[0] <= 1e-6, (i, it)
+    assert same >= 3, same
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_jcqp", [1.0, 2.0])
+def test_reference_call_protocol_use_jcqp_all_stance_n16(cm, use_jcqp):
+    """use_jcqp == 2 (and 1) at the deployed N = 16 with every foot in stance
+    (n = 192) must return the solved forces through get_solution, not zeros."""
+    solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+    solver_mod.load_library()
+    N = 16
+    prm = cm.make_params(N)
+    rec = cm.make_instances(1, N, random_contact_frac=0.0)[0]
+    gait = np.ones(4 * N, np.int32)
+    recs = cm.pack_records(rec[None, 0:3], rec[None, 3:6], rec[None, 6:10], rec[None, 10:13],
+                           rec[None, 13:25], rec[None, 32:32 + 12 * N], gait[None],
+                           rpy=rec[None, 25:28], x_drag=rec[None, 28:29])
+    from oracle import oracle as orc
+    if not orc.ref_available():
+        pytest.skip("oracle/_ref not present")
+    q, st_ref, _ = orc.ref_solve_batch(recs, prm, nthreads=1)
+    try:
+        solver_mod.setup_problem(0.026, N, 0.4, 120)
+        solver_mod.update_x_drag(float(rec[28]))
+        solver_mod.update_solver_settings(TIGHT["max_iter"], TIGHT["rho"], TIGHT["sigma"],
+                                          TIGHT["alpha"], TIGHT["terminate"], use_jcqp)
+        solver_mod.update_problem_data_floats(rec[0:3], rec[3:6], rec[6:10], rec[10:13],
+                                              rec[13:25], rec[25], rec[26], rec[27],
+                                              np.array(prm.weights), rec[32:32 + 12 * N],
+                                              prm.alpha, gait)
+        sol = np.array([solver_mod.get_solution(j) for j in range(12 * N)])
+    finally:
+        solver_mod.update_solver_settings(100, 1e-7, 1e-8, 1.5, 1e-5, 0)
+    assert np.abs(sol[2::3]).max() > 1.0          # stance fz, not zeros
+    assert rel_force_err(sol[None], q)[0] <= 1e-4
 
 
 @pytest.mark.gpu

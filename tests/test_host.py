@@ -46,6 +46,15 @@ def test_generator_deterministic_and_shaped(cm):
     assert not np.array_equal(a, cm.make_instances(64, 10, seed=43))
 
 
+def test_philox_known_answer(cm):
+    """Philox4x32-10 of the per-instance generator against the Random123 known-answer vectors
+    (counter 0, key 0 and counter/key all ones)."""
+    import importlib
+    ins = importlib.import_module("quad-periodic-mpc_amd.instances")
+    out = ins.philox4x32(np.array([0]), np.array([0]), 1)[0]
+    assert [int(x) for x in out] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+
+
 def test_trot_table_matches_gait_rule(cm):
     """OffsetDurationGait::getMpcTable (Gait.cpp:159-188), trot P=18."""
     it = np.arange(18)
