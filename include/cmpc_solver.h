@@ -104,11 +104,22 @@
 #define CMPC_LOCO_GAIT     41  /* int32: OffsetDurationGait P, offsets[4], durations[4]        */
 #define CMPC_LOCO_FLAGS    50  /* state, uint32: CMPC_LOCO_OMNI | STANDING | PRONK | FIRST     */
 #define CMPC_LOCO_STAND    51  /* stand_traj x, y, yaw (:146-151; stand_traj[0], [1], [5])     */
-#define CMPC_LOCO_WORDS    56
+/* foot placement and swing (:276-331, :350-402; FootSwingTrajectory.cpp:17-42)                  */
+#define CMPC_LOCO_SWREM    56  /* state: swingTimeRemaining[4] (:287-296)                       */
+#define CMPC_LOCO_SWST     60  /* out: gait->getSwingState() of the tick (Gait.cpp:102-135)      */
+#define CMPC_LOCO_P0       64  /* state: footSwingTrajectories[l]._p0 [4][3] (:262, :378)       */
+#define CMPC_LOCO_PF       76  /* state: footSwingTrajectories[l]._pf [4][3], the foothold Pf   */
+#define CMPC_LOCO_PDES     88  /* state: footSwingTrajectories[l]._p [4][3] = pDesFootWorld     */
+#define CMPC_LOCO_WORDS    104
 #define CMPC_LOCO_OMNI     1u  /* omniMode: v_des is already in the world frame (:211)         */
 #define CMPC_LOCO_STANDING 2u  /* current_gait == 4: stand trajectory (:527-533)               */
 #define CMPC_LOCO_PRONK    4u  /* gaitNumber == 8 (pacing): roll compensation off (:230)      */
 #define CMPC_LOCO_FIRST    8u  /* firstRun: world_position_desired = position (:249-256)       */
+#define CMPC_LOCO_SIMFEET  16u /* simulator feet (not in the reference): after each tick a     */
+                               /* swinging foot is at its pDesFootWorld, a foot entering stance */
+                               /* touches down (z = 0) and stance feet stay fixed in the world; */
+                               /* cmpc_batch_rollout then leaves the feet alone                 */
+#define CMPC_LOCO_FSWING0  256u/* firstSwing[l] is bit (8 + l) (:75, :289, :376, :413)          */
 
 /* Batch-shared controller constants. */
 typedef struct cmpc_loco_params {
@@ -116,6 +127,12 @@ typedef struct cmpc_loco_params {
   int   iters_between_mpc;/* _iterationsBetweenMPC                                             */
   float x_drag_gain;      /* _dyn_params->cmpc_x_drag                                          */
   int   pad;
+  float hip_x, hip_y;     /* quadruped._abadLocation x, y: getHipLocation(l) = (+-x, +-y, 0)    */
+                          /* (Quadruped.h:95-102; A1: 0.1805, 0.047, MiniCheetah.h:30-31)       */
+  float abad_link;        /* quadruped._abadLinkLength (A1: 0.0838)                             */
+  float swing_height;     /* _dyn_params->Swing_traj_height (ros_config.yaml:62: 0.17)          */
+  float bonus_swing;      /* _dyn_params->cmpc_bonus_swing (ros_config.yaml:70: 0)              */
+  float pad2[3];
 } cmpc_loco_params;
 
 /* Per-instance status (batched API). The reference has no status: on qpOASES failure it prints

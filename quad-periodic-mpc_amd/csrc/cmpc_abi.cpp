@@ -232,7 +232,9 @@ extern "C" int cmpc_batch_assemble(cmpc_batch* h, float* d_loco, const cmpc_loco
     g_last_error = "cmpc_batch_assemble: bad arguments";
     return -1;
   }
-  cmpc::LocoParams kp{lp->dt, lp->iters_between_mpc, lp->x_drag_gain, h->kp.N, h->kp.rec_words};
+  cmpc::LocoParams kp{lp->dt,        lp->iters_between_mpc, lp->x_drag_gain,  h->kp.N,
+                      h->kp.rec_words, lp->hip_x,            lp->hip_y,        lp->abad_link,
+                      lp->swing_height, lp->bonus_swing};
   hipError_t e = cmpc::launch_assemble(d_loco, kp, d_records, d_due, batch, h->stream);
   if (e != hipSuccess) return fail("launch_assemble", e);
   return 0;
@@ -245,7 +247,7 @@ extern "C" int cmpc_batch_rollout(cmpc_batch* h, float* d_loco, const float* d_r
     g_last_error = "cmpc_batch_rollout: bad arguments";
     return -1;
   }
-  cmpc::LocoParams kp{h->kp.dt, 1, 0.f, h->kp.N, h->kp.rec_words};
+  cmpc::LocoParams kp{h->kp.dt, 1, 0.f, h->kp.N, h->kp.rec_words, 0.f, 0.f, 0.f, 0.f, 0.f};
   hipError_t e = cmpc::launch_rollout(d_loco, d_records, d_forces, d_xi6, d_due, kp, h->kp.dt,
                                       batch, h->stream);
   if (e != hipSuccess) return fail("launch_rollout", e);

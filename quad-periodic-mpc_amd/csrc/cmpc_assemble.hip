@@ -11,11 +11,14 @@
 //   v_des_world             :210-211  rBody^T v_des_robot (omniMode: v_des_robot)
 //   rpy_int / rpy_comp      :218-230  integral pitch / roll compensation, clamped to +-0.25
 //   world_position_desired  :237-257  += dt v_des_world (not standing); first run: = position
+//   foot placement          :276-331  swingTimeRemaining, Raibert / capture-point foothold Pf with
+//                           the pfx_rel / pfy_rel clamps, interleave offsets, yaw correction
 //   iterationCounter++      :334
 //   getMpcTable             Gait.cpp:159-188 (rows i < N; periodic for N > P)
 //   updateMPCIfNeeded       :511-586  every `iters` ticks: the trajAll reference
 //   solveDenseMPC inputs    :619-633, :786-790, :806-818  p = (x, y, z_groundtruth), r = pFoot - p,
 //                           x_drag = x_comp_integral, then the x_comp_integral update
+//   swing / stance          :337-431  getSwingState, firstSwing, Bezier pDesFootWorld
 // and, when an MPC step is due, writes the instance's solve record (include/cmpc_solver.h) for
 // cmpc_batch_solve: the record the reference would hand to update_problem_data_floats.
 //
@@ -94,10 +97,71 @@ __global__ __launch_bounds__(256) void cmpc_assemble_kernel(float* __restrict__ 
     wy += dt * vdw1;
   }
   uint32_t nflags = flags;
+  float pfoot[4][3];
+#pragma unroll
+  for (int l = 0; l < 4; l++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) pfoot[l][k] = s[CMPC_LOCO_PFOOT + 3 * l + k];
   if (flags & CMPC_LOCO_FIRST) {
     wx = pos0;
     wy = pos1;
     nflags &= ~(uint32_t)CMPC_LOCO_FIRST;
+    // :258-271 setInitialPosition / setFinalPosition(pFoot[i])
+#pragma unroll
+    for (int t = 0; t < 12; t++) {
+      s[CMPC_LOCO_P0 + t] = pfoot[t / 3][t % 3];
+      s[CMPC_LOCO_PF + t] = pfoot[t / 3][t % 3];
+    }
+  }
+
+  // foot placement (:276-331): swingTimeRemaining and the foothold Pf of every leg
+  const int off[4] = {__float_as_int(s[CMPC_LOCO_GAIT + 1]), __float_as_int(s[CMPC_LOCO_GAIT + 2]),
+                      __float_as_int(s[CMPC_LOCO_GAIT + 3]), __float_as_int(s[CMPC_LOCO_GAIT + 4])};
+  const int dur[4] = {__float_as_int(s[CMPC_LOCO_GAIT + 5]), __float_as_int(s[CMPC_LOCO_GAIT + 6]),
+                      __float_as_int(s[CMPC_LOCO_GAIT + 7]), __float_as_int(s[CMPC_LOCO_GAIT + 8])};
+  const float dtm0 = dt * (float)iters;                  // recompute_timing (:95-99, :207)
+  const float swing_time = dtm0 * (float)(P - dur[0]);   // Gait.cpp:252-256 (_swing)
+  const float stance_time = dtm0 * (float)dur[0];        // Gait.cpp:263-267 (_stance)
+  {
+    const float R00 = 1.f - 2.f * (e2 * e2 + e3 * e3), R01 = 2.f * (e1 * e2 - e0 * e3),
+                R02 = 2.f * (e1 * e3 + e0 * e2);
+    const float R10 = 2.f * (e1 * e2 + e0 * e3), R11 = 1.f - 2.f * (e1 * e1 + e3 * e3),
+                R12 = 2.f * (e2 * e3 - e0 * e1);
+    const float side[4] = {-1.f, 1.f, -1.f, 1.f};
+    const float ily[4] = {-0.08f, 0.08f, 0.02f, -0.02f};
+    const float igain = -0.2f;
+    const float v_abs = fabsf(vdx);
+    const float th = -yaw_rate * stance_time / 2.f;      // coordinateRotation(Z, th) (:307)
+    // sin / cos through double, rounded once: the correctly rounded float (glibc's sinf / cosf
+    // are correctly rounded too), so the kernel and the oracle agree bit for bit
+    const float cth = (float)cos((double)th), sth = (float)sin((double)th);
+    const float hz = 0.5f * pos2 / 9.81f;
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      float swrem = s[CMPC_LOCO_SWREM + l];
+      swrem = (flags & (CMPC_LOCO_FSWING0 << l)) ? swing_time : swrem - dt;
+      s[CMPC_LOCO_SWREM + l] = swrem;
+      const float hx = (l == 0 || l == 1) ? lp.hip_x : -lp.hip_x;
+      const float hy = (l == 1 || l == 3) ? lp.hip_y : -lp.hip_y;
+      float prf0 = hx + 0.f, prf1 = hy + side[l] * lp.abad_link, prf2 = 0.f + 0.f;
+      prf1 = prf1 + ily[l] * v_abs * igain;
+      const float py0 = cth * prf0 + sth * prf1 + 0.f * prf2;
+      const float py1 = -sth * prf0 + cth * prf1 + 0.f * prf2;
+      const float py2 = 0.f * prf0 + 0.f * prf1 + 1.f * prf2;
+      const float t0 = py0 + vdx * swrem, t1 = py1 + vdy * swrem, t2 = py2 + 0.f * swrem;
+      const float pf0 = pos0 + (R00 * t0 + R01 * t1 + R02 * t2);
+      const float pf1 = pos1 + (R10 * t0 + R11 * t1 + R12 * t2);
+      // :318-322; the double literals promote the first terms to double
+      float pfx = (float)((double)vw0 * (0.5 + (double)lp.bonus_swing) * (double)stance_time +
+                          (double)(0.03f * (vw0 - vdw0)) + (double)(hz * (vw1 * yaw_rate)));
+      float pfy = (float)((double)vw1 * 0.5 * (double)stance_time * (double)dtm0 +
+                          (double)(0.03f * (vw1 - vdw1)) + (double)(hz * (-vw0 * yaw_rate)));
+      pfx = fminf(fmaxf(pfx, -0.3f), 0.3f);
+      pfy = fminf(fmaxf(pfy, -0.3f), 0.3f);
+      s[CMPC_LOCO_PF + 3 * l + 0] = pf0 + pfx;
+      s[CMPC_LOCO_PF + 3 * l + 1] = pf1 + pfy;
+      s[CMPC_LOCO_PF + 3 * l + 2] = 0.f;
+    }
   }
 
   // iterationCounter++ (:334); updateMPCIfNeeded (:514) tests the incremented counter
@@ -185,6 +249,57 @@ __global__ __launch_bounds__(256) void cmpc_assemble_kernel(float* __restrict__ 
   }
   s[CMPC_LOCO_WPD + 0] = wx;
   s[CMPC_LOCO_WPD + 1] = wy;
+
+  // swing / stance of each foot (:337-338, :350-431): getSwingState (Gait.cpp:102-135) at the
+  // phase of setIterations (Gait.cpp:218-226, pre-increment counter), then the Bezier swing
+  // (FootSwingTrajectory.cpp:17-42, Interpolation.h:30-37)
+  const float phase = (float)(counter % (iters * P)) / (float)(iters * P);
+#pragma unroll
+  for (int l = 0; l < 4; l++) {
+    const float offf = (float)off[l] / (float)P, durf = (float)dur[l] / (float)P;
+    float so = offf + durf;
+    if (so > 1.f) so = so - 1.f;
+    const float sd = 1.f - durf;
+    float prog = phase - so;
+    if (prog < 0.f) prog = prog + 1.f;
+    prog = (prog >= sd) ? 0.f : prog / sd;
+    s[CMPC_LOCO_SWST + l] = prog;
+    const uint32_t fbit = CMPC_LOCO_FSWING0 << l;
+    const bool first_before = (nflags & fbit) != 0u;
+    if (prog > 0.f) {
+      float a[3];
+      if (first_before) {
+        nflags &= ~fbit;
+#pragma unroll
+        for (int k = 0; k < 3; k++) { a[k] = pfoot[l][k]; s[CMPC_LOCO_P0 + 3 * l + k] = a[k]; }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) a[k] = s[CMPC_LOCO_P0 + 3 * l + k];
+      }
+      const float b0 = s[CMPC_LOCO_PF + 3 * l + 0], b1 = s[CMPC_LOCO_PF + 3 * l + 1],
+                  b2 = s[CMPC_LOCO_PF + 3 * l + 2];
+      const float x = prog;
+      const float bez = x * x * x + 3.f * (x * x * (1.f - x));
+      float pd0 = a[0] + bez * (b0 - a[0]);
+      float pd1 = a[1] + bez * (b1 - a[1]);
+      float u, y0, yf;
+      if (x < 0.5f) { u = x * 2.f; y0 = a[2]; yf = a[2] + lp.swing_height; }
+      else { u = x * 2.f - 1.f; y0 = a[2] + lp.swing_height; yf = b2; }
+      const float bz = u * u * u + 3.f * (u * u * (1.f - u));
+      const float pd2 = y0 + bz * (yf - y0);
+      s[CMPC_LOCO_PDES + 3 * l + 0] = pd0;
+      s[CMPC_LOCO_PDES + 3 * l + 1] = pd1;
+      s[CMPC_LOCO_PDES + 3 * l + 2] = pd2;
+      if (flags & CMPC_LOCO_SIMFEET) {
+        s[CMPC_LOCO_PFOOT + 3 * l + 0] = pd0;
+        s[CMPC_LOCO_PFOOT + 3 * l + 1] = pd1;
+        s[CMPC_LOCO_PFOOT + 3 * l + 2] = pd2;
+      }
+    } else {
+      nflags |= fbit;  // firstSwing = true (:413)
+      if ((flags & CMPC_LOCO_SIMFEET) && !first_before) s[CMPC_LOCO_PFOOT + 3 * l + 2] = 0.f;
+    }
+  }
   s[CMPC_LOCO_FLAGS] = __uint_as_float(nflags);
   due[i] = mpc ? 1 : 0;
 }
@@ -197,9 +312,10 @@ __global__ __launch_bounds__(256) void cmpc_assemble_kernel(float* __restrict__ 
 // SolverMPC.cpp:607-615):
 //   x+ = Adt x0 + Bdt u0 + Qdt xi,  Qdt = dt Q + dt^2/2 A Q + dt^3/6 A^2 Q (A^3 = 0),
 // with x0 = [rpy, p, w, v, -9.8] from the record. The new rpy / p / w / v are written back to
-// the controller state (quaternion from ZYX Euler angles, z_groundtruth = p_z). The feet move
-// with the body in x and y (footstep relocation is not simulated: each foot keeps its offset
-// from the body, on the ground). One thread per instance.
+// the controller state (quaternion from ZYX Euler angles, z_groundtruth = p_z). Feet: with
+// CMPC_LOCO_SIMFEET the assemble kernel moves them (swing feet on their Bezier trajectory, touch
+// down at the foothold Pf, stance feet fixed in the world) and the rollout leaves them alone;
+// without it they keep their offset from the body in x and y. One thread per instance.
 __global__ __launch_bounds__(256) void cmpc_rollout_kernel(float* __restrict__ loco,
                                                            const float* __restrict__ recs,
                                                            const float* __restrict__ forces,
@@ -273,10 +389,12 @@ __global__ __launch_bounds__(256) void cmpc_rollout_kernel(float* __restrict__ l
     s[CMPC_LOCO_VW + k] = x1[9 + k];
   }
   s[CMPC_LOCO_ZGT] = x1[5];
+  if (!(__float_as_uint(s[CMPC_LOCO_FLAGS]) & CMPC_LOCO_SIMFEET)) {
 #pragma unroll
-  for (int l = 0; l < 4; l++) {
-    s[CMPC_LOCO_PFOOT + 3 * l + 0] += x1[3] - x0[3];
-    s[CMPC_LOCO_PFOOT + 3 * l + 1] += x1[4] - x0[4];
+    for (int l = 0; l < 4; l++) {
+      s[CMPC_LOCO_PFOOT + 3 * l + 0] += x1[3] - x0[3];
+      s[CMPC_LOCO_PFOOT + 3 * l + 1] += x1[4] - x0[4];
+    }
   }
   // ZYX Euler -> quaternion (w, x, y, z)
   const float cr = cosf(0.5f * x1[0]), sr = sinf(0.5f * x1[0]);

@@ -27,6 +27,7 @@ struct LocoParams {
   float x_drag_gain;
   int horizon;
   int rec_words;
+  float hip_x, hip_y, abad_link, swing_height, bonus_swing;  // foot placement (cmpc_loco_params)
 };
 
 // Scratch ints needed by launch_solve for max_batch instances.

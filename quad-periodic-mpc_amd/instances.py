@@ -244,7 +244,8 @@ def loco_gaits(P: int = 18):
 
 def make_loco_states(batch: int, seed: int = BASE_SEED + 11, P: int = 18, first_run_frac: float = 0.1,
                      gaits=("trotting", "trotting", "trotting", "bounding", "pronking", "galloping",
-                            "standing", "walking", "pacing"), omni_frac: float = 0.1) -> np.ndarray:
+                            "standing", "walking", "pacing"), omni_frac: float = 0.1,
+                     sim_feet_frac: float = 0.0) -> np.ndarray:
     """Locomotion-controller states [batch, LOCO_WORDS] (include/cmpc_solver.h CMPC_LOCO_*):
     A1-like body states, world foot positions around the nominal stance, stick commands, a
     random gait from ``gaits`` at a random iteration counter, and warm integrator states."""
@@ -304,4 +305,13 @@ def make_loco_states(batch: int, seed: int = BASE_SEED + 11, P: int = 18, first_
     s[:, LOCO_STAND] = pos[:, 0]
     s[:, LOCO_STAND + 1] = pos[:, 1]
     s[:, LOCO_STAND + 2] = yaw
+    # swing state (:276-331, :350-431): a swing in progress from / towards the current feet
+    from .records import LOCO_FSWING0, LOCO_P0, LOCO_PDES, LOCO_PF, LOCO_SIMFEET, LOCO_SWREM
+    s[:, LOCO_SWREM:LOCO_SWREM + 4] = g.uniform(0.0, 0.25, (B, 4))
+    for w in (LOCO_P0, LOCO_PF, LOCO_PDES):
+        s[:, w:w + 12] = s[:, LOCO_PFOOT:LOCO_PFOOT + 12]
+    fs = (g.random((B, 4)) < 0.5).astype(np.uint32)
+    flags = flags | (fs * (LOCO_FSWING0 << np.arange(4, dtype=np.uint32))).sum(1).astype(np.uint32)
+    flags[g.random(B) < sim_feet_frac] |= LOCO_SIMFEET
+    s[:, LOCO_FLAGS] = flags.view(np.float32)
     return s

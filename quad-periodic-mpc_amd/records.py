@@ -35,19 +35,32 @@ STATUS_NAMES = {0: "ok", 1: "max_iter", 2: "infeasible", 3: "not_pd", 4: "bad_in
 LOCO_POS, LOCO_ZGT, LOCO_Q, LOCO_RPY, LOCO_VW, LOCO_WW, LOCO_PFOOT = 0, 3, 4, 8, 11, 14, 17
 LOCO_CMD, LOCO_HEIGHT, LOCO_VDES, LOCO_WPD, LOCO_RPYINT, LOCO_XCI = 29, 32, 33, 35, 37, 39
 LOCO_COUNTER, LOCO_GAIT, LOCO_FLAGS, LOCO_STAND = 40, 41, 50, 51
-LOCO_WORDS = 56
-LOCO_OMNI, LOCO_STANDING, LOCO_PRONK, LOCO_FIRST = 1, 2, 4, 8
+LOCO_SWREM, LOCO_SWST, LOCO_P0, LOCO_PF, LOCO_PDES = 56, 60, 64, 76, 88
+LOCO_WORDS = 104
+LOCO_OMNI, LOCO_STANDING, LOCO_PRONK, LOCO_FIRST, LOCO_SIMFEET = 1, 2, 4, 8, 16
+LOCO_FSWING0 = 256          # firstSwing[l] = bit 8 + l
+LOCO_FSWING_ALL = 0xF00
+
+# A1 geometry (MiniCheetah.h:30-37, Quadruped.h:95-102) and swing parameters (ros_config.yaml:62,70)
+A1_HIP_X, A1_HIP_Y, A1_ABAD_LINK = 0.1805, 0.047, 0.0838
+SWING_HEIGHT, BONUS_SWING = 0.17, 0.0
 
 
 class LocoParams(ctypes.Structure):
     """cmpc_loco_params (include/cmpc_solver.h)."""
     _fields_ = [("dt", ctypes.c_float), ("iters_between_mpc", ctypes.c_int),
-                ("x_drag_gain", ctypes.c_float), ("pad", ctypes.c_int)]
+                ("x_drag_gain", ctypes.c_float), ("pad", ctypes.c_int),
+                ("hip_x", ctypes.c_float), ("hip_y", ctypes.c_float),
+                ("abad_link", ctypes.c_float), ("swing_height", ctypes.c_float),
+                ("bonus_swing", ctypes.c_float), ("pad2", ctypes.c_float * 3)]
 
 
-def make_loco_params(dt: float = 0.002, iters_between_mpc: int = 13,
-                     x_drag_gain: float = 0.0) -> LocoParams:
-    return LocoParams(dt, iters_between_mpc, x_drag_gain, 0)
+def make_loco_params(dt: float = 0.002, iters_between_mpc: int = 13, x_drag_gain: float = 0.0,
+                     hip_x: float = A1_HIP_X, hip_y: float = A1_HIP_Y,
+                     abad_link: float = A1_ABAD_LINK, swing_height: float = SWING_HEIGHT,
+                     bonus_swing: float = BONUS_SWING) -> LocoParams:
+    return LocoParams(dt, iters_between_mpc, x_drag_gain, 0, hip_x, hip_y, abad_link,
+                      swing_height, bonus_swing)
 
 
 def record_words(horizon: int) -> int:
