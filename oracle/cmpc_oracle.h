@@ -76,6 +76,16 @@ void oracle_residual(const float* log, const float* rec, float f_ext[6]);
 float oracle_est_step(float* state, float f3, float t, int* use_f_est);
 
 
+/* QuadProg++ solve_quadprog restatement (quadprog_oracle.c, built into _build/libqp_oracle.so
+ * with -ffp-contract=off). Returns the CMPC_* status; fval = +inf when infeasible. */
+int oracle_quadprog(int n, int p, int m, const double* G, int ldg, const double* g0,
+                    const double* CE, int ldce, const double* ce0, const double* CI, int ldci,
+                    const double* ci0, int max_iter, double* x, double* fval, int* iters_out);
+void oracle_quadprog_batch(int batch, int n_max, int p_max, int m_max, const int32_t* dims,
+                           const double* G, const double* g0, const double* CE, const double* ce0,
+                           const double* CI, const double* ci0, int max_iter, double* x,
+                           double* fval, uint8_t* status, int32_t* iters);
+
 #ifdef __cplusplus
 }
 #endif

@@ -488,3 +488,67 @@ def assemble_tick(loco: np.ndarray, horizon: int, dt: float, iters: int, x_drag_
                 s[R_.LOCO_PFOOT + 3 * i + 2] = z0             # touchdown
     s.view(np.uint32)[R_.LOCO_FLAGS] = flags
     return s, rec
+
+
+# ---------------------------------------------------------------------------------------------
+# QuadProg++ solve_quadprog restatement (quadprog_oracle.c), the WBIC QP (WBIC.cpp:91)
+# ---------------------------------------------------------------------------------------------
+QP_SO = os.path.join(HERE, "_build", "libqp_oracle.so")
+_qp = None
+
+
+def qp_lib():
+    global _qp
+    if _qp is None:
+        if not os.path.exists(QP_SO):
+            build()
+        _qp = ctypes.CDLL(QP_SO)
+        _qp.oracle_quadprog_batch.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p] * 7 + \
+            [ctypes.c_int] + [ctypes.c_void_p] * 4
+    return _qp
+
+
+def quadprog_batch(G, g0, CE, ce0, CI, ci0, dims=None, max_iter: int = 1000):
+    """-> (x [B,n_max], f [B], status [B] u8, iters [B] i32); fp64 blocks as cmpc_batch_quadprog."""
+    arrs = [np.ascontiguousarray(a, np.float64) for a in (G, g0, CE, ce0, CI, ci0)]
+    B, n = arrs[0].shape[0], arrs[0].shape[-1]
+    p, m = arrs[3].shape[-1], arrs[5].shape[-1]
+    dm = None if dims is None else np.ascontiguousarray(dims, np.int32)
+    x = np.zeros((B, n))
+    f = np.zeros(B)
+    st = np.zeros(B, np.uint8)
+    it = np.zeros(B, np.int32)
+    qp_lib().oracle_quadprog_batch(B, n, p, m, None if dm is None else dm.ctypes.data,
+                                   *[a.ctypes.data for a in arrs], int(max_iter), x.ctypes.data,
+                                   f.ctypes.data, st.ctypes.data, it.ctypes.data)
+    return x, f, st, it
+
+
+def qp_kkt(G, g0, CE, ce0, CI, ci0, x, n, p, m, act_tol=1e-7):
+    """KKT certificate of one solution (independent of any solver): multipliers of the
+    equalities and the (numerically) active inequalities by non-negative least squares on the
+    stationarity condition G x + g0 = CE lam + CI_A mu, mu >= 0. -> dict of residuals (stationarity, primal equality,
+    primal inequality violation, most negative inequality multiplier), all scaled."""
+    G, g0 = G[:n, :n], g0[:n]
+    CE, ce0, CI, ci0 = CE[:n, :p], ce0[:p], CI[:n, :m], ci0[:m]
+    x = x[:n]
+    s = CI.T @ x + ci0
+    scale = max(1.0, np.abs(s).max() if m else 1.0, np.abs(ci0).max() if m else 1.0)
+    act = np.nonzero(np.abs(s) <= act_tol * scale)[0]
+    grad = G @ x + g0
+    M = np.concatenate([CE, CI[:, act]], 1)
+    gscale = max(1.0, np.abs(G).max() * np.abs(x).max(), np.abs(g0).max())
+    if M.shape[1]:
+        # non-negative multipliers for the inequalities (lambda = lp - lm free), so degenerate
+        # vertices with more active constraints than variables still certify
+        from scipy.optimize import nnls
+        K = np.concatenate([CE, -CE, CI[:, act]], 1)
+        mult, _ = nnls(K, grad, maxiter=50 * K.shape[1])
+        res = grad - K @ mult
+        mu = mult[2 * p:]
+    else:
+        res, mu = grad, np.zeros(0)
+    return dict(stationarity=np.abs(res).max() / gscale,
+                eq=(np.abs(CE.T @ x + ce0).max() / scale) if p else 0.0,
+                ineq=(max(0.0, -s.min()) / scale) if m else 0.0,
+                dual=(max(0.0, -mu.min()) / gscale) if mu.size else 0.0)

@@ -21,7 +21,7 @@ OBJ = os.path.join(ROOT, "build", "obj")
 SOURCES = ["cmpc_class1.hip", "cmpc_class2_w80.hip", "cmpc_class2_w96.hip", "cmpc_class2_w128.hip",
            "cmpc_wide_w80.hip", "cmpc_wide_w96.hip", "cmpc_wide_w128.hip", "cmpc_wide_w192.hip",
            "cmpc_wide_w256.hip", "cmpc_classg.hip", "cmpc_launch.hip", "cmpc_estimator.hip", "cmpc_assemble.hip",
-           "cmpc_admm.hip", "cmpc_abi.cpp"]
+           "cmpc_admm.hip", "cmpc_quadprog.hip", "cmpc_abi.cpp"]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: the SLP pass packs adjacent row updates into v_pk_fma_f32, which ties
 # slot registers into 64-bit pairs and made the register-resident rows spill

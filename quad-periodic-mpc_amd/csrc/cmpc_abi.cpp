@@ -82,6 +82,9 @@ static void gauss_kernel(float sigma, int radius, float* out) {
 }
 
 extern "C" const char* cmpc_last_error(void) { return g_last_error.c_str(); }
+namespace cmpc {
+void set_last_error(const char* msg) { g_last_error = msg; }  // for the other translation units
+}  // namespace cmpc
 
 // the general class needs 2 (12N)^2 floats per workgroup of its persistent grid
 static int ensure_gscratch(cmpc_batch* h) {

@@ -59,6 +59,10 @@ int main(int argc, char** argv) {
       t[8] = 0.2f;
       t[9] = 0.5f;
     }
+    // the ROS node's inputs of the periodic-disturbance estimator (SolverMPC.cpp:692-798):
+    // simulation time and the measured vertical disturbance, a 1.3 Hz sine here
+    simulation_time = dt * c;
+    f_ext[3] = 5.f * std::sin(2.f * 3.14159265f * 1.3f * simulation_time);
     const auto t0 = std::chrono::steady_clock::now();
     setup_problem(dt, N, 0.4, 120);
     update_x_drag(0.1f);

@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
     "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing", "cmpc_batch_estimate",
     "cmpc_batch_assemble", "cmpc_batch_rollout", "cmpc_batch_admm",
+    "cmpc_batch_quadprog",   # include/cmpc_quadprog.h
 )
 
 _lib = None
@@ -106,6 +107,8 @@ def load_library(path: str = LIB_PATH):
     lib.cmpc_batch_rollout.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_int]
+    lib.cmpc_batch_quadprog.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int] + \
+        [ctypes.c_void_p] * 7 + [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int]
     _lib = lib
     return lib
 
@@ -301,6 +304,19 @@ class BatchSolver:
             batch = loco.shape[0]
         _check(self.lib.cmpc_batch_rollout(self._h, _ptr(loco), _ptr(records), _ptr(forces),
                                            _ptr(xi6), _ptr(due), int(batch)), "cmpc_batch_rollout")
+
+    def quadprog(self, G, g0, CE, ce0, CI, ci0, x, f, status, iters=None, dims=None,
+                 max_iter: int = 1000, batch: int | None = None) -> None:
+        """Batched QuadProg++ ``solve_quadprog`` on device (``cmpc_batch_quadprog``,
+        include/cmpc_quadprog.h): fp64 blocks G [B,n,n], g0 [B,n], CE [B,n,p], ce0 [B,p],
+        CI [B,n,m], ci0 [B,m]; optional per-instance ``dims`` [B,3] int32 (n, p, m)."""
+        if batch is None:
+            batch = G.shape[0]
+        n, p, m = int(G.shape[-1]), int(ce0.shape[-1]), int(ci0.shape[-1])
+        _check(self.lib.cmpc_batch_quadprog(self._h, n, p, m, _ptr(dims), _ptr(G), _ptr(g0),
+                                            _ptr(CE), _ptr(ce0), _ptr(CI), _ptr(ci0), int(max_iter),
+                                            _ptr(x), _ptr(f), _ptr(status), _ptr(iters), int(batch)),
+               "cmpc_batch_quadprog")
 
     def enable_timing(self, steps: int) -> None:
         """Record HIP events around each size-class launch of the next ``steps`` solves."""

@@ -79,8 +79,10 @@ def test_library_exports_header_symbols(cm):
     for sym in solver.EXPORTED_SYMBOLS:
         assert sym in names, sym
     # every prototype in the header is among the exports
-    hdr = open(os.path.join(ROOT, "include", "cmpc_solver.h")).read()
+    hdr = "".join(open(os.path.join(ROOT, "include", h)).read()
+                  for h in sorted(os.listdir(os.path.join(ROOT, "include"))) if h.endswith(".h"))
     protos = re.findall(r"CMPC_EXTERNC\s+[\w\s\*]+?\b(\w+)\s*\(", hdr)
+    assert "cmpc_batch_quadprog" in protos
     for p in protos:
         assert p in names, p
     lib = ctypes.CDLL(path)  # loads without a GPU
