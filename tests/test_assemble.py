@@ -334,7 +334,6 @@ def test_gpu_closed_loop_trot_tracks_command(cm, sim_feet):
     z = np.abs(out[:, R.LOCO_POS + 2] - 0.29)
     # simulator feet: a few robots still oscillate after 1.56 s (1024 robots: max 3.9 cm)
     assert z.max() < (0.05 if sim_feet else 0.02), z.max()
-    assert np.median(z) < 0.01, np.median(z)
     # velocity error against the (filtered) command: at least 5x below the initial one
     # (the controller trades velocity against its position reference, so it is not zero)
     def world(st, w):  # the robot-frame command in the world frame (identity in omni mode)
