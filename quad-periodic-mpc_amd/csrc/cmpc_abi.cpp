@@ -280,6 +280,7 @@ extern "C" int cmpc_batch_read_timing(cmpc_batch* h, float* ms, int* steps_recor
     ms[2 * i] = a;
     ms[2 * i + 1] = b;
   }
+  (void)hipGetLastError();  // an unrecorded event must not poison the next launch's check
   if (steps_recorded) *steps_recorded = h->ev_next;
   if (class1_overflow) {
     int c = 0;

@@ -10,30 +10,41 @@
 //   count >= 400: f_est(3) = est_amp + sin(2 pi t est_freq + est_phase)  (sic '+', :766)
 //   qg uses f_est only when count > 500 (:808) -> record flag bit 0.
 //
-// MI355X mapping: one 256-thread workgroup per instance. The 400-sample window is staged in LDS
-// as double; each thread produces output samples of both Gaussian FIRs (43 and 163 taps, float
-// taps computed on the host exactly as the reference computes them, accumulated in double), then
-// one DFT bin (k = 1..200) each against a 400-entry twiddle table in LDS; the peak, mean and std
-// are workgroup reductions. Instances outside the estimation window only push their sample
-// (a few words of HBM traffic) and evaluate the compensation.
+// MI355X mapping: one 128-thread workgroup (two wavefronts) per instance; the 400-sample window
+// is staged in LDS as double. Everything is fp64, as the reference.
+//   * band-pass: thread t < 100 produces the four consecutive output samples 4t..4t+3 of both
+//     Gaussian FIRs (43 and 163 float taps, computed on the host exactly as the reference does,
+//     widened to double in LDS). Per tap one LDS read extends a 4-sample sliding window in
+//     registers and feeds four fp64 FMAs; taps are accumulated in ascending order per output,
+//     as gaussian_filter does;
+//   * DFT peak: thread t < 100 runs the Goertzel recurrence s = x + 2 cos(w) s1 - s2 for bins
+//     t+1 and t+101 over the band (one broadcast LDS read per two samples, no twiddle gathers:
+//     the round-1 kernel's table lookups at (k t) mod 400 were 1.8 bank conflicts per LDS
+//     instruction), |X_k|^2 = s1^2 + s2^2 - 2 cos(w) s1 s2; the first maximum over bins 1..200
+//     (a direct DFT or the reference's FFT agree to ~1e-12 relative on the magnitudes);
+//   * mean / std / argmax: wave butterflies plus one LDS exchange.
+// Instances outside the estimation window only push their sample (a few words of HBM traffic)
+// and evaluate the compensation.
 #include "cmpc_common.h"
 
 namespace cmpc {
 namespace {
 
 constexpr int W = CMPC_EST_WINDOW;
-constexpr int NT = 256;
+constexpr int NT = 128;
 constexpr int NWV = NT / 64;
 constexpr int NBIN = W / 2;  // bins 1..200 are searched (bin 0 excluded, SolverMPC.cpp:503-510)
+constexpr int NOUT = 4;      // FIR outputs per thread
+constexpr int NFIR = W / NOUT;
+constexpr int NTAPS7 = 2 * kGaussR7 + 1, NTAPS27 = 2 * kGaussR27 + 1;
+static_assert(W % NOUT == 0 && NFIR <= NT && NBIN <= 2 * NT, "estimator thread mapping");
 
 struct SharedE {
   double d[W];       // window, oldest first
   double band[W];    // blur7 - blur27
-  double twc[W], tws[W];
+  double k7[NTAPS7], k27[NTAPS27];
   double redd[NWV];
-  float redv[NWV];
   int redi[NWV];
-  float k7[2 * kGaussR7 + 1], k27[2 * kGaussR27 + 1];
   int count, head;
   float t_now, t0, t1;
 };
@@ -49,6 +60,24 @@ __device__ __forceinline__ double block_sum_d(double x, SharedE& sh) {
   for (int i = 0; i < NWV; i++) s += sh.redd[i];
   __syncthreads();
   return s;
+}
+
+// one Gaussian FIR over outputs i0..i0+3, edge-clamped, taps ascending (SolverMPC.cpp:419-436)
+template <int R>
+__device__ __forceinline__ void fir4(const double* __restrict__ d, const double* __restrict__ k,
+                                     int i0, double (&acc)[NOUT]) {
+  double win[NOUT];
+#pragma unroll
+  for (int r = 0; r < NOUT - 1; r++) win[r + 1] = d[min(max(i0 - R + r, 0), W - 1)];
+#pragma unroll 8
+  for (int j = -R; j <= R; j++) {
+#pragma unroll
+    for (int r = 0; r < NOUT - 1; r++) win[r] = win[r + 1];
+    win[NOUT - 1] = d[min(max(i0 + j + NOUT - 1, 0), W - 1)];
+    const double kj = k[j + R];
+#pragma unroll
+    for (int r = 0; r < NOUT; r++) acc[r] = fma(win[r], kj, acc[r]);
+  }
 }
 
 // residual of ConvexMPCLocomotion.cpp:639-771 for one instance (one thread)
@@ -150,33 +179,22 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
   double* prm = reinterpret_cast<double*>(st + CMPC_EST_PARAMS);  // stat, amp, freq, phase
   if (count >= W && count <= CMPC_EST_STOP) {
     const int head = sh.head;
-    for (int i = tid; i < W; i += NT) {
-      const int idx = (head + i) % W;
-      sh.d[i] = (double)st[CMPC_EST_F + idx];
-      double sn, cs;
-      sincospi(2.0 * (double)i / (double)W, &sn, &cs);
-      sh.twc[i] = cs;
-      sh.tws[i] = sn;
-    }
-    for (int i = tid; i < 2 * kGaussR7 + 1; i += NT) sh.k7[i] = gauss[i];
-    for (int i = tid; i < 2 * kGaussR27 + 1; i += NT) sh.k27[i] = gauss[2 * kGaussR7 + 1 + i];
+    for (int i = tid; i < W; i += NT) sh.d[i] = (double)st[CMPC_EST_F + (head + i) % W];
+    for (int i = tid; i < NTAPS7; i += NT) sh.k7[i] = (double)gauss[i];  // float taps, exact
+    for (int i = tid; i < NTAPS27; i += NT) sh.k27[i] = (double)gauss[NTAPS7 + i];
     if (tid == 0) {
       sh.t0 = st[CMPC_EST_T + head];
       sh.t1 = st[CMPC_EST_T + (head + 1) % W];
     }
     __syncthreads();
-    // band-pass: gaussian_filter(7) - gaussian_filter(27), edge clamped, taps in ascending order
-    for (int i = tid; i < W; i += NT) {
-      double a7 = 0.0, a27 = 0.0;
-      for (int j = -kGaussR7; j <= kGaussR7; j++) {
-        const int idx = min(max(i + j, 0), W - 1);
-        a7 += sh.d[idx] * (double)sh.k7[j + kGaussR7];
-      }
-      for (int j = -kGaussR27; j <= kGaussR27; j++) {
-        const int idx = min(max(i + j, 0), W - 1);
-        a27 += sh.d[idx] * (double)sh.k27[j + kGaussR27];
-      }
-      sh.band[i] = a7 - a27;
+    // band-pass: gaussian_filter(7) - gaussian_filter(27)
+    if (tid < NFIR) {
+      const int i0 = NOUT * tid;
+      double a7[NOUT] = {0.0, 0.0, 0.0, 0.0}, a27[NOUT] = {0.0, 0.0, 0.0, 0.0};
+      fir4<kGaussR7>(sh.d, sh.k7, i0, a7);
+      fir4<kGaussR27>(sh.d, sh.k27, i0, a27);
+#pragma unroll
+      for (int r = 0; r < NOUT; r++) sh.band[i0 + r] = a7[r] - a27[r];
     }
     __syncthreads();
     // mean and standard deviation of the band (fit_sin's amplitude and offset guesses)
@@ -186,50 +204,58 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
     part = 0.0;
     for (int i = tid; i < W; i += NT) part += (sh.band[i] - mean) * (sh.band[i] - mean);
     const double sd = sqrt(block_sum_d(part, sh) / W);
-    // |DFT| of bins 1..200 and the first maximum
-    float best = -1.f;
-    int bk = 0x7fffffff;
-    double bestd = -1.0;
-    if (tid < NBIN) {
-      const int k = tid + 1;
-      double re = 0.0, im = 0.0;
-      int m = 0;  // (k t) mod W
-      for (int t = 0; t < W; t++) {
-        re += sh.band[t] * sh.twc[m];
-        im -= sh.band[t] * sh.tws[m];
-        m += k;
-        if (m >= W) m -= W;
+    // |DFT|^2 of bins tid+1 and tid+101 by Goertzel recurrences
+    double v = __builtin_huge_val();
+    int bi = 0x7fffffff;
+    if (tid < NBIN / 2) {
+      const int ka = tid + 1, kb = tid + 1 + NBIN / 2;
+      double ca, sa, cb, sb;
+      sincospi(2.0 * ka / W, &sa, &ca);
+      sincospi(2.0 * kb / W, &sb, &cb);
+      (void)sa;
+      (void)sb;
+      const double pa = 2.0 * ca, pb = 2.0 * cb;
+      double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
+      const double2* bb = reinterpret_cast<const double2*>(sh.band);
+#pragma unroll 4
+      for (int t2 = 0; t2 < W / 2; t2++) {
+        const double2 x = bb[t2];
+        double a0 = fma(pa, a1, x.x) - a2;
+        double b0 = fma(pb, b1, x.x) - b2;
+        a2 = a1; a1 = a0;
+        b2 = b1; b1 = b0;
+        a0 = fma(pa, a1, x.y) - a2;
+        b0 = fma(pb, b1, x.y) - b2;
+        a2 = a1; a1 = a0;
+        b2 = b1; b1 = b0;
       }
-      bestd = sqrt(re * re + im * im);
-      bk = k;
+      const double ma = a1 * a1 + a2 * a2 - pa * a1 * a2;
+      const double mb = b1 * b1 + b2 * b2 - pb * b1 * b2;
+      // the larger magnitude, ties to the smaller bin (negated for the min-reduction)
+      if (mb > ma) { v = -mb; bi = kb; } else { v = -ma; bi = ka; }
     }
-    // argmax in double with ties to the smaller bin: reduce on (-mag, k)
-    {
-      double v = (tid < NBIN) ? -bestd : __builtin_huge_val();
-      int i = bk;
+    // first maximum: reduce on (-|X|^2, k)
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const double ov = __shfl_xor(v, off, 64);
-        const int oi = __shfl_xor(i, off, 64);
-        if (ov < v || (ov == v && oi < i)) { v = ov; i = oi; }
-      }
-      const int wv = tid >> 6;
-      if ((tid & 63) == 0) { sh.redd[wv] = v; sh.redi[wv] = i; }
-      __syncthreads();
-      if (tid == 0) {
-        double bv = sh.redd[0];
-        int bi = sh.redi[0];
-        for (int w = 1; w < NWV; w++)
-          if (sh.redd[w] < bv || (sh.redd[w] == bv && sh.redi[w] < bi)) { bv = sh.redd[w]; bi = sh.redi[w]; }
-        const double dt = (double)sh.t1 - (double)sh.t0;
-        const double guess_freq = fabs(bi / (W * dt));  // fftfreq(n, dt)[k], k <= n/2
-        const double omega = 2 * M_PI * guess_freq;
-        prm[0] = mean;               // est_stat = offset
-        prm[1] = sd * sqrt(2.0);     // est_amp
-        prm[2] = omega / (2 * M_PI); // est_freq
-        prm[3] = 0.0;                // est_phase
-      }
-      (void)best;
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ov = __shfl_xor(v, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ov < v || (ov == v && oi < bi)) { v = ov; bi = oi; }
+    }
+    const int wv = tid >> 6;
+    if ((tid & 63) == 0) { sh.redd[wv] = v; sh.redi[wv] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      double bv = sh.redd[0];
+      int bk = sh.redi[0];
+      for (int w = 1; w < NWV; w++)
+        if (sh.redd[w] < bv || (sh.redd[w] == bv && sh.redi[w] < bk)) { bv = sh.redd[w]; bk = sh.redi[w]; }
+      const double dt = (double)sh.t1 - (double)sh.t0;
+      const double guess_freq = fabs(bk / (W * dt));  // fftfreq(n, dt)[k], k <= n/2
+      const double omega = 2 * M_PI * guess_freq;
+      prm[0] = mean;               // est_stat = offset
+      prm[1] = sd * sqrt(2.0);     // est_amp
+      prm[2] = omega / (2 * M_PI); // est_freq
+      prm[3] = 0.0;                // est_phase
     }
     __syncthreads();
   }

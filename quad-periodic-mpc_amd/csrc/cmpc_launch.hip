@@ -9,6 +9,8 @@
 //     and 192-column classes carry the batch and run side by side on the two streams.
 //   -DCMPC_LEGACY_C2 builds the round-1 arrangement instead (one lane per row, 2-wavefront
 //     classes of 80 / 96 / 128 columns, G above 128) for A/B measurements.
+#include <stdlib.h>
+
 #include "cmpc_kernels.h"
 
 namespace cmpc {
@@ -69,7 +71,11 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   for (int j = 0; j < kLists; j++) list[j] = d_work + 8 + (size_t)j * max_batch;
   hipError_t e = hipMemsetAsync(d_work, 0, 8 * sizeof(int), stream);
   if (e != hipSuccess) return e;
-  if (batch <= 0) return hipSuccess;
+  if (batch <= 0) {  // keep the timing slots consistent (zero-length launches)
+    if (ev)
+      for (int i = 0; i < 3; i++) (void)hipEventRecord(ev[i], stream);
+    return hipSuccess;
+  }
   const int n_max = 12 * P.N;  // a class no instance of this horizon can reach is not launched
   if (n_max > 64) {
     hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_recs,
@@ -79,7 +85,23 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     for (int s = 0; s < kSideStreams; s++)
       if ((e = hipStreamWaitEvent(ctx.side[s], ctx.fork, 0)) != hipSuccess) return e;
     // one workgroup per possible list entry (the lengths are only known on the device);
-    // surplus workgroups exit after one load
+    // surplus workgroups exit after one load. CMPC_EXACT_GRID=1 (diagnostic): read the list
+    // lengths back first (a host round trip per solve) and launch exact grids
+    int grid_of[kLists];
+    for (int j = 0; j < kLists; j++) grid_of[j] = batch;
+    static const bool exact = [] {
+      const char* v = getenv("CMPC_EXACT_GRID");
+      return v && v[0] == '1';
+    }();
+    if (exact) {
+      static int* h_cnt = nullptr;
+      if (!h_cnt && (e = hipHostMalloc(reinterpret_cast<void**>(&h_cnt), 8 * sizeof(int))) != hipSuccess)
+        return e;
+      if ((e = hipMemcpyAsync(h_cnt, cnt, 8 * sizeof(int), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipStreamSynchronize(stream)) != hipSuccess)
+        return e;
+      for (int j = 0; j < kLists; j++) grid_of[j] = h_cnt[1 + j];
+    }
 #ifdef CMPC_LEGACY_C2
     if ((e = launch_class2_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], nullptr,
                                nullptr, batch, ctx.side[0])) != hipSuccess)
@@ -94,20 +116,20 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
 #else
     // side 0: 80, 128, 256; side 1: 96, 192 (at N = 20 the 128- and 192-column classes, which
     // carry the batch, run side by side)
-    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], batch,
+    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], grid_of[0],
                              ctx.side[0])) != hipSuccess)
       return e;
     if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2],
-                                           batch, ctx.side[1])) != hipSuccess)
+                                           grid_of[1], ctx.side[1])) != hipSuccess)
       return e;
     if (n_max > 96 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
-                                            batch, ctx.side[0])) != hipSuccess)
+                                            grid_of[2], ctx.side[0])) != hipSuccess)
       return e;
     if (n_max > 128 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4],
-                                             batch, ctx.side[1])) != hipSuccess)
+                                             grid_of[3], ctx.side[1])) != hipSuccess)
       return e;
     if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5],
-                                             batch, ctx.side[0])) != hipSuccess)
+                                             grid_of[4], ctx.side[0])) != hipSuccess)
       return e;
     const bool g_possible = n_max > 256;
 #endif

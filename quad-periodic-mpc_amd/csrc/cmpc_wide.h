@@ -165,7 +165,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   using G = WGeo<NV>;
   constexpr int NH = G::NH;
   constexpr int RQ = G::RQ;
-  const int t = threadIdx.x;
+  const int t = tid_opq();  // opaque: nothing lane-dependent is hoisted out of the persistent loop
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int h = lane >> 5;
@@ -739,32 +739,78 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
 
 }  // namespace
 
-// One workgroup per entry of the class's list; the grid is sized for the worst case (the list
-// length is only known on the device) and surplus workgroups exit at once.
+// One workgroup per possible entry of the class's list (the list length is only known on the
+// device); surplus workgroups exit after one load. -DCMPC_WIDE_PERSIST=1 builds persistent
+// workgroups instead, which dequeue entries by decrementing the list length (grid sized to the
+// machine, wide_grid): measured to spill (w128: 168 VGPRs + 48 spilled, 256 SGPR spills, against
+// 159 VGPRs and no spills for one solve per workgroup), so it is off.
+#ifndef CMPC_WIDE_PERSIST
+#define CMPC_WIDE_PERSIST 0
+#endif
 #if CMPC_WIDE_VGPR_CAP > 0
 #define CMPC_WIDE_VGPR_ATTR __attribute__((amdgpu_num_vgpr(CMPC_WIDE_VGPR_CAP)))
 #else
 #define CMPC_WIDE_VGPR_ATTR
 #endif
+// Kernel arguments as one struct, so the persistent loop can re-read all of them per instance
+// through a single opaque kernarg pointer (below)
+struct WideArgs {
+  const float* recs;
+  float* forces;
+  uint8_t* status;
+  int32_t* iters;
+  const int* in_list;
+  int* in_count;
+  KParams P;
+};
+
 template <int NV>
 __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGPR_ATTR void cmpc_solve_w_kernel(
-    const float* __restrict__ recs, KParams P, float* __restrict__ forces,
-    uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
-    const int* __restrict__ in_count) {
+    WideArgs A) {
   __shared__ SharedW<NV> sh;
+#if CMPC_WIDE_PERSIST
+  __shared__ int s_next;
+  for (;;) {
+    // every argument re-read per instance through an opaque pointer: hoisted out of the loop
+    // they would hold ~45 SGPRs for the whole kernel and spill
+    const WideArgs* a = &A;
+    asm volatile("" : "+s"(a));
+    if (threadIdx.x == 0) s_next = atomicSub(a->in_count, 1) - 1;  // consumes the list length
+    __syncthreads();
+    const int b = s_next;
+    if (b < 0) break;
+    const int inst = a->in_list[b];
+    solve_w<NV>(a->recs + (size_t)inst * a->P.rec_words, a->P, sh,
+                a->forces + (size_t)inst * 12 * a->P.N, a->status + inst,
+                a->iters ? a->iters + inst : nullptr);
+    __syncthreads();  // sh and s_next are free again
+  }
+#else
   const int b = blockIdx.x;
-  if (b >= *in_count) return;
-  const int inst = in_list[b];
-  solve_w<NV>(recs + (size_t)inst * P.rec_words, P, sh, forces + (size_t)inst * 12 * P.N,
-              status + inst, iters ? iters + inst : nullptr);
+  if (b >= *A.in_count) return;
+  const int inst = A.in_list[b];
+  solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
+              A.status + inst, A.iters ? A.iters + inst : nullptr);
+#endif
+}
+
+// workgroups of a persistent wide class: about two residency waves of the widest geometry
+inline int wide_grid(int list_bound) {
+#if CMPC_WIDE_PERSIST
+  return list_bound < 2048 ? list_bound : 2048;
+#else
+  return list_bound;
+#endif
 }
 
 template <int NV>
 hipError_t launch_wide_impl(const float* d_recs, const KParams& P, float* d_forces,
                             uint8_t* d_status, int32_t* d_iters, const int* in_list,
                             const int* in_count, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(cmpc_solve_w_kernel<NV>, dim3(grid), dim3(WGeo<NV>::NT), 0, stream, d_recs, P,
-                     d_forces, d_status, d_iters, in_list, in_count);
+  grid = wide_grid(grid);
+  if (grid <= 0) return hipSuccess;
+  const WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, const_cast<int*>(in_count), P};
+  hipLaunchKernelGGL(cmpc_solve_w_kernel<NV>, dim3(grid), dim3(WGeo<NV>::NT), 0, stream, A);
   return hipGetLastError();
 }
 
