@@ -196,6 +196,154 @@ def plumbing_solve(N):
     return fn
 
 
+def local_leg(args, cm, prm, config, N, B, steps, warmup, dev, rank, barrier, sync, dist,
+              frac=None):
+    """Configs 2 / 3 / 5 on this rank: inputs resident in HBM, ``warmup`` untimed steps, then
+    ``steps`` timed ones bracketed by barrier + synchronize, max over ranks. -> dict."""
+    import torch
+    frac = args.random_contact_frac if frac is None else frac
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    recs_np = cm.make_instances(B, N, random_contact_frac=frac, first_id=rank * B)
+    recs = torch.from_numpy(recs_np).to(dev)
+    forces = torch.empty((B, 12 * N), dtype=torch.float32, device=dev)
+    status = torch.empty(B, dtype=torch.uint8, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    solver = None
+    est = est0 = None
+    if args.dry_run:
+        fn = plumbing_solve(N)
+
+        def step():
+            fn(recs, forces, status)
+    else:
+        solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
+        solver = solver_mod.BatchSolver(prm, max_batch=B, stream=torch.cuda.current_stream(dev))
+
+        def step():
+            solver.solve(recs, forces, status, iters)
+
+        if config == 5:
+            R = importlib.import_module("quad-periodic-mpc_amd.records")
+            est_np, logs_np = _config5_state(cm, R, recs_np, B)
+            est0 = torch.from_numpy(est_np).to(dev)
+            est = est0.clone()
+            logs = torch.from_numpy(logs_np).to(dev)
+            t_next = [10.4]
+
+            def step():  # noqa: F811  (config 5: estimator step, then the solve)
+                solver.estimate(est, recs, logs=logs, sim_time=t_next[0])
+                t_next[0] += prm.dt
+                solver.solve(recs, forces, status, iters)
+
+    sync()
+    for _ in range(warmup):
+        step()
+    if config == 5 and est is not None:  # restart the histories at 400 samples for the timed steps
+        sync()
+        est.copy_(est0)
+        t_next[0] = 10.4
+    sync()
+    if solver is not None:
+        solver.enable_timing(steps)
+    # ---- timed region: K steps, bracketed by barrier + synchronize on both sides ----------
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return dict(elapsed=elapsed, solver=solver, forces=forces, status=status, iters=iters,
+                recs=recs, recs_np=recs_np, world=world)
+
+
+def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
+    """roofline object of the dominant launch (see the module docstring / DESIGN.md §5)."""
+    if not launch_ms.size:
+        return None
+    fl = algorithmic_flops(N)
+    c1 = launch_ms[:, 0]
+    c2 = launch_ms[:, 1]
+    units1 = units_per_launch - ovf
+    t1 = float(np.mean(c1)) * 1e-3
+    wide = units1 < units_per_launch // 2   # at N >= 16 the wide classes carry the batch
+    if wide:
+        # whole solve (class 1 + the concurrently running wide classes) as one launch
+        t1 = float(np.mean(c1 + c2)) * 1e-3
+        units1 = units_per_launch
+    achieved = fl * units1 / t1 / 1e12 if t1 > 0 else None
+    traffic, pmc = load_pmc(N, units_per_launch, "cmpc_solve_c1_kernel" if not wide else "cmpc_solve_w_kernel<128>")
+    roofline = {
+        "bound": "valu",
+        "achieved": round(achieved, 3) if achieved else None,
+        "peak": FP32_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / FP32_PEAK_TFLOPS, 5) if achieved else None,
+        "traffic": traffic,
+        "kernel": ("cmpc_solve_c1_kernel (n <= 64 class, one wavefront per instance)" if not wide
+                   else "whole solve: every size class, concurrent streams"),
+        "units_per_launch": int(units1),
+        "flops_per_unit": fl,
+        "avg_launch_ms": round(t1 * 1e3, 4),
+        "class1_avg_launch_ms": round(float(np.mean(c1)), 4),
+        "tail_avg_ms": round(float(np.mean(c2)), 4),
+        "wide_class_units": int(ovf),
+        "hbm_bytes_per_unit": algorithmic_bytes(N, config == 5),
+        "hbm_gbs": round(algorithmic_bytes(N, config == 5) * value / 1e9, 3),
+        "note": "FP32 VALU roof (the path is latency/VALU-bound, not HBM: ~1300 FLOP/B). "
+                "achieved = SURVEY §8(d) F(N) (dense reference algorithm) x instances of "
+                "the launch / its HIP-event time on the solver stream; the kernels execute "
+                "fewer flops (reduced n, structured condensation), so frac is speed against "
+                "the reference's work. valu_pmc: counters of the same kernel (profiles/"
+                "pmc_summary.json); valu_issue_util = VALU instructions x 2 cycles (wave64 on "
+                "SIMD-32) / (1024 SIMDs x 2.4 GHz x launch time)",
+    }
+    if pmc:
+        vp = {k: pmc[k] for k in ("valu_insts_per_wave", "lds_insts_per_wave", "waves",
+                                   "lds_bank_conflict_frac", "wait_frac", "issue_stall_frac",
+                                   "active_frac", "vgpr", "scratch", "pmc_tag") if k in pmc}
+        if "valu_insts_per_wave" in pmc and "waves" in pmc and t1 > 0:
+            vp["valu_issue_util"] = round(pmc["valu_insts_per_wave"] * pmc["waves"] * 2.0 /
+                                          (1024 * 2.4e9 * t1), 4)
+        roofline["valu_pmc"] = vp
+    return roofline
+
+
+def other_configs(args, cm, dev, rank, barrier, sync, dist):
+    """BASELINE configs 2 and 5 measured in the same (default, 1-GPU) run, after config 3, with
+    the same protocol: resident inputs, warmup, barrier + synchronize, HIP-event roofline."""
+    out = {}
+    for config, N, B, steps, warmup in ((2, 10, 4096, 200, 20), (5, 20, 65536, 5, 2)):
+        prm = cm.make_params(N)
+        leg = local_leg(args, cm, prm, config, N, B, steps, warmup, dev, rank, barrier, sync, dist)
+        launch_ms, ovf = leg["solver"].read_timing()
+        value = B * steps / leg["elapsed"]
+        st = np.bincount(leg["status"].cpu().numpy(), minlength=5)
+        d = {"metric": METRIC_C2 if config == 2 else METRIC_C5, "value": round(value, 1),
+             "unit": "QP solves/s", "ms_per_step": round(leg["elapsed"] / steps * 1e3, 4),
+             "steps": steps, "warmup": warmup, "batch": B, "horizon": N,
+             "roofline": make_roofline(launch_ms, ovf, B, N, value, config),
+             "status_counts": {cm.STATUS_NAMES[i]: int(c) for i, c in enumerate(st) if c},
+             "forces_digest": digest(leg["forces"])}
+        if config == 5:
+            d["workload"] = ("N=20, per step one batched periodic-disturbance estimator step "
+                             "(LogData residual, Gaussian band-pass, DFT sine fit) fused ahead of "
+                             "the solve, histories at 400..405 samples")
+            if not args.no_cpu_baseline:
+                d["cpu_baseline"] = cpu_baseline(prm, N, config5=True)
+        else:
+            d["workload"] = "N=10, batch 4096 (same instance mix as config 3)"
+            d["cpu_baseline"] = "same per-instance workload as config 3: see cpu_baseline"
+        leg["solver"].close()
+        out[f"config{config}"] = d
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -269,69 +417,37 @@ def main():
 
         def step():
             pipe.step(recs_root)
+
+        sync()
+        for _ in range(args.warmup):
+            step()
+        sync()
+        timed = None if args.dry_run else pipe._solver
+        units_per_launch = max(pipe.sizes)
+        if timed is not None:
+            timed.enable_timing(args.steps * pipe.chunks)
+        # ---- timed region: K steps, bracketed by barrier + synchronize on both sides ------
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
     else:
         B = args.batch or (4096 if config == 2 else 65536)
+        leg = local_leg(args, cm, prm, config, N, B, args.steps, args.warmup, dev, rank, barrier,
+                        sync, dist)
+        elapsed, timed, units_per_launch = leg["elapsed"], leg["solver"], B
+        forces, status, recs_np, solver = leg["forces"], leg["status"], leg["recs_np"], leg["solver"]
+        iters = leg["iters"]
+        recs = leg["recs"]
         B_total, B_local = B * world, B
-        recs_np = cm.make_instances(B, N, random_contact_frac=args.random_contact_frac,
-                                    first_id=rank * B)
-        recs = torch.from_numpy(recs_np).to(dev)
-        forces = torch.empty((B, 12 * N), dtype=torch.float32, device=dev)
-        status = torch.empty(B, dtype=torch.uint8, device=dev)
-        iters = torch.empty(B, dtype=torch.int32, device=dev)
-        if args.dry_run:
-            fn = plumbing_solve(N)
-
-            def step():
-                fn(recs, forces, status)
-        else:
-            solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
-            solver = solver_mod.BatchSolver(prm, max_batch=B, stream=torch.cuda.current_stream(dev))
-
-            def step():
-                solver.solve(recs, forces, status, iters)
-
-            if config == 5:
-                R = importlib.import_module("quad-periodic-mpc_amd.records")
-                est_np, logs_np = _config5_state(cm, R, recs_np, B)
-                est0 = torch.from_numpy(est_np).to(dev)
-                est = est0.clone()
-                logs = torch.from_numpy(logs_np).to(dev)
-                t_next = [10.4]
-
-                def step():  # noqa: F811  (config 5: estimator step, then the solve)
-                    solver.estimate(est, recs, logs=logs, sim_time=t_next[0])
-                    t_next[0] += prm.dt
-                    solver.solve(recs, forces, status, iters)
-
-    sync()
-    for _ in range(args.warmup):
-        step()
-    if config == 5:  # restart the histories at 400 samples for the timed steps
-        sync()
-        est.copy_(est0)
-        t_next[0] = 10.4
-    sync()
-    timed = solver
-    units_per_launch = B_local
-    if config == 4 and not args.dry_run:
-        timed = pipe._solver
-        units_per_launch = max(pipe.sizes)
-    if timed is not None:
-        timed.enable_timing(args.steps * (pipe.chunks if config == 4 else 1))
-
-    # ---- timed region: K steps, bracketed by barrier + synchronize on both sides ----------
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     # ---- untimed extras -------------------------------------------------------------------
     launch_ms, ovf = (timed.read_timing() if timed is not None else (np.zeros((0, 2)), 0))
@@ -374,6 +490,10 @@ def main():
                         "per step (PCIe-inclusive; not `value`)"}
     if config == 3 and not args.dry_run and not args.no_extras and world == 1:
         extras["abi_latency"] = abi_latency()
+        if solver is not None:
+            solver.close()
+            solver = None
+        extras["other_configs"] = other_configs(args, cm, dev, rank, barrier, sync, dist)
     status_counts = None
     if st_local is not None:
         sc = np.bincount(st_local.cpu().numpy(), minlength=5)
@@ -391,47 +511,7 @@ def main():
 
     value = B_total * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    fl = algorithmic_flops(N)
-    roofline = None
-    if launch_ms.size:
-        c1 = launch_ms[:, 0]
-        c2 = launch_ms[:, 1]
-        units1 = units_per_launch - ovf
-        t1 = float(np.mean(c1)) * 1e-3
-        wide = units1 < units_per_launch // 2   # at N >= 16 the wide classes carry the batch
-        if wide:
-            # whole solve (class 1 + the concurrently running wide classes) as one launch
-            t1 = float(np.mean(c1 + c2)) * 1e-3
-            units1 = units_per_launch
-        achieved = fl * units1 / t1 / 1e12 if t1 > 0 else None
-        traffic, pmc = load_pmc(N, units_per_launch, "cmpc_solve_c1_kernel" if not wide else "cmpc_solve_w")
-        roofline = {
-            "bound": "valu",
-            "achieved": round(achieved, 3) if achieved else None,
-            "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_PEAK_TFLOPS, 5) if achieved else None,
-            "traffic": traffic,
-            "kernel": ("cmpc_solve_c1_kernel (n <= 64 class, one wavefront per instance)" if not wide
-                       else "whole solve: every size class, concurrent streams"),
-            "units_per_launch": int(units1),
-            "flops_per_unit": fl,
-            "avg_launch_ms": round(t1 * 1e3, 4),
-            "class1_avg_launch_ms": round(float(np.mean(c1)), 4),
-            "tail_avg_ms": round(float(np.mean(c2)), 4),
-            "wide_class_units": int(ovf),
-            "hbm_bytes_per_unit": algorithmic_bytes(N, config == 5),
-            "hbm_gbs": round(algorithmic_bytes(N, config == 5) * value / 1e9, 3),
-            "note": "FP32 VALU roof (the path is latency/VALU-bound, not HBM: ~1300 FLOP/B). "
-                    "achieved = SURVEY §8(d) F(N) (dense reference algorithm) x instances of "
-                    "the launch / its HIP-event time on the solver stream; the kernels execute "
-                    "fewer flops (reduced n, structured condensation), so frac is speed against "
-                    "the reference's work; measured VALU utilisation is in valu_pmc",
-        }
-        if pmc:
-            roofline["valu_pmc"] = {k: pmc[k] for k in ("valu_busy", "valu_insts_per_launch",
-                                                       "lds_bank_conflict_frac", "vgpr",
-                                                       "scratch", "pmc_tag") if k in pmc}
+    roofline = make_roofline(launch_ms, ovf, units_per_launch, N, value, config)
 
     cpu = None
     if not args.no_cpu_baseline and world == 1 and not args.dry_run:

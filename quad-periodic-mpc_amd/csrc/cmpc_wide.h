@@ -29,6 +29,9 @@
 #pragma once
 #include "cmpc_common.h"
 
+#ifndef CMPC_DIAG_STOP
+#define CMPC_DIAG_STOP 0
+#endif
 #ifndef CMPC_WIDE_WAVES_PER_EU
 #define CMPC_WIDE_WAVES_PER_EU 3
 #endif
@@ -360,6 +363,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   if (h == 0 && r < NV) sh.ybuf[r & 1][r >> 1] = yv;
   wbar();
 
+#if CMPC_DIAG_STOP != 1  // diagnostic builds: stop after the Cholesky (1) / after J (2)
   // ---- J = L^-T: row r solves L x = e_r over its half of the columns (LDS reads only; the
   // pivot value x_k lives in the half holding column k: one partner exchange per step)
   static_for<0, NH>([&](auto J) {
@@ -391,6 +395,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     }
   });
 
+#endif
   // ---- unconstrained minimiser x = -J y
   float xv;
   {
@@ -420,7 +425,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   int p = -1;
   Cons cp{};
   float up = 0.f;
-  if (status == CMPC_OK) {
+  if (status == CMPC_OK && CMPC_DIAG_STOP == 0) {
     for (;;) {
       wpin(slot);
       const int t = tid_opq();

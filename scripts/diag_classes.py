@@ -20,21 +20,24 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--frac", type=float, default=0.25)
     a = ap.parse_args()
     import torch
     cm = importlib.import_module("quad-periodic-mpc_amd")
     sm = importlib.import_module("quad-periodic-mpc_amd.solver")
     N, B = a.horizon, a.batch
-    recs_np = cm.make_instances(B, N, seed=20251015)
+    ap2 = a
+    recs_np = cm.make_instances(B, N, random_contact_frac=ap2.frac)
     gait = cm.unpack_gait(recs_np, N)
     n = 3 * (gait != 0).sum(1)
+    torch.cuda.set_stream(torch.cuda.Stream())
     recs = torch.from_numpy(recs_np).cuda()
     f = torch.empty((B, 12 * N), device="cuda")
     st = torch.empty(B, dtype=torch.uint8, device="cuda")
     it = torch.empty(B, dtype=torch.int32, device="cuda")
     for cap in (100, 1, 0):
         prm = cm.make_params(N, max_iter=cap)
-        s = sm.BatchSolver(prm, max_batch=B)
+        s = sm.BatchSolver(prm, max_batch=B, stream=torch.cuda.current_stream())
         s.solve(recs, f, st, it)
         torch.cuda.synchronize()
         s.enable_timing(a.reps)

@@ -5,7 +5,7 @@ and the full estimate -> solve pipeline against the reference qpOASES forces (fi
 tests/golden/n20_config5.npz, made by tests/golden/make_golden.py config5).
 
 Tolerances: flags and the moment compensation starts are exact; f_est(3) within 1e-5 relative
-(double-precision filters and DFT on both sides, summation orders differ); forces 2e-4 as the
+(double-precision filters and DFT on both sides, summation orders differ); forces 1e-4 as the
 other N = 20 sets (tests/test_gpu_parity.py)."""
 import importlib
 
@@ -87,7 +87,7 @@ def test_config5_pipeline_forces_match_reference(cm, solver_mod, on_stream):
     s.close()
     assert (status.cpu().numpy() == 0).all()
     err = rel_force_err(forces.cpu().numpy(), g["q_ref"])
-    assert err.max() <= 2e-4, (err.max(), int(err.argmax()))
+    assert err.max() <= 1e-4, (err.max(), int(err.argmax()))
 
 
 def test_device_residual_matches_oracle(cm, solver_mod, on_stream):

@@ -3,8 +3,10 @@ the committed qpOASES golden fixtures and, where oracle/_ref travelled with the 
 reference pipeline run live on the same seeded inputs.
 
 Tolerance (north_star): ground-reaction forces within 1e-4 relative to qpOASES, norm-wise per
-instance: |f - f_ref|_inf / max(|f_ref|_inf, 1 N) <= 1e-4 (horizon 20: 2e-4, where the
-reference's own fp32 condensation noise alone reaches ~7e-5).
+instance: |f - f_ref|_inf / max(|f_ref|_inf, 1 N) <= 1e-4 at every horizon, N = 20 included
+(round 1 allowed 2e-4 there; measured with the two-lane wide classes: golden sets <= 5.7e-5,
+live N = 20 batches <= 9.2e-5, scripts/parity_report.py; the reference's own fp32 condensation
+differs from an fp64 one by up to ~7e-5 at N = 20).
 """
 import importlib
 
@@ -17,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 
 def tol_for(N):
-    return 2e-4 if N >= 20 else 1e-4
+    return 1e-4
 
 
 @pytest.fixture(scope="module")
