@@ -142,6 +142,71 @@ def qpoases(H, g, A, lb, ub, nwsr_max: int = 100):
     return x[:n], nw.value, ri.value, r2
 
 
+def ct_mats64(rec: np.ndarray):
+    """Independent float64 restatement of ct_ss_mats (SolverMPC.cpp:260-279) with the
+    RobotState model (RobotState.cpp:9-50): (A_c, B_c, Q_c)."""
+    q = rec[6:10].astype(np.float64)
+    w_, x, y, z = q
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w_ * z), 2 * (x * z + w_ * y)],
+                  [2 * (x * y + w_ * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w_ * x)],
+                  [2 * (x * z - w_ * y), 2 * (y * z + w_ * x), 1 - 2 * (x * x + y * y)]])
+    Iw = R @ np.diag([.07, .26, .242]) @ R.T
+    Ii = np.linalg.inv(Iw)
+    r = rec[13:25].reshape(3, 4).astype(np.float64)
+    A = np.zeros((13, 13)); B = np.zeros((13, 12))
+    A[3, 9] = A[4, 10] = A[5, 11] = A[11, 12] = 1.0
+    A[11, 9] = rec[28]
+    A[0:3, 6:9] = R.T
+    for b in range(4):
+        rx = np.array([[0, -r[2, b], r[1, b]], [r[2, b], 0, -r[0, b]], [-r[1, b], r[0, b], 0]])
+        B[6:9, 3 * b:3 * b + 3] = Ii @ rx
+        B[9:12, 3 * b:3 * b + 3] = np.eye(3) / 12.0
+    Q = np.zeros((13, 6)); Q[6:12] = np.eye(6)
+    return A, B, Q
+
+
+def fp64_solve(rec: np.ndarray, prm):
+    """The reference pipeline in float64 throughout: scipy expm discretisation, dense condensation
+    (SolverMPC.cpp:806-814), the same swing elimination, qpOASES on the float64 reduced QP.
+    Returns (q_soln [12N], qpOASES return value). This is the optimum the reference's fp32
+    pipeline approximates; at N = 20 the reference itself lands up to ~1e-4 (relative) from it
+    (scripts/exact_gap.py)."""
+    from scipy.linalg import expm
+    N = prm.horizon
+    c = condense(rec, prm, full=False)
+    A, B, Q = ct_mats64(rec)
+    M = np.zeros((31, 31))
+    M[:13, :13] = A; M[:13, 13:25] = B; M[:13, 25:31] = Q
+    E = expm(prm.dt * M)
+    Ad, Bd, Qd = E[:13, :13], E[:13, 13:25], E[:13, 25:31]
+    x0 = c["x0"].astype(np.float64)
+    nx, nu = 13 * N, 12 * N
+    Bqp = np.zeros((nx, nu)); Aqp = np.zeros((nx, 13)); Qqp = np.zeros((nx, 6))
+    P = [np.eye(13)]
+    for _ in range(N):
+        P.append(Ad @ P[-1])
+    for r in range(N):
+        Aqp[13 * r:13 * r + 13] = P[r + 1]
+        for cc in range(r + 1):
+            Bqp[13 * r:13 * r + 13, 12 * cc:12 * cc + 12] = P[r - cc] @ Bd
+            Qqp[13 * r:13 * r + 13] += P[r - cc] @ Qd
+    w = np.tile(np.array(list(prm.weights) + [0.0]), N)
+    Xd = np.zeros(nx)
+    Xd.reshape(N, 13)[:, :12] = rec[32:32 + 12 * N].reshape(N, 12)
+    f = np.zeros(6)
+    if int(np.ascontiguousarray(rec[30:31], np.float32).view(np.uint32)[0]) & 1:
+        f[3] = rec[29]
+    qH = 2 * (Bqp.T @ (w[:, None] * Bqp) + prm.alpha * np.eye(nu))
+    qg = 2 * Bqp.T @ (w * (Aqp @ x0 + Qqp @ f - Xd))
+    red = reduce(rec, prm, qH.astype(np.float32), qg.astype(np.float32))
+    keep = ~red["var_elim"]
+    x, _, ri, _ = qpoases(qH[np.ix_(keep, keep)], qg[keep], red["A"], red["lb"], red["ub"],
+                          nwsr_max=1000)
+    out = np.zeros(nu)
+    out[keep] = x
+    return out, ri
+
+
 def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1):
     """Reference pipeline over a batch -> (q_soln [B, 12N] f64, status [B], nWSR [B])."""
     B = records.shape[0]

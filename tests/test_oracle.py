@@ -8,34 +8,12 @@ from scipy.linalg import expm
 from conftest import GOLDEN_SETS, golden_params, load_golden, rel_force_err
 
 
-def _ct_mats(rec, x0_rpy=None):
-    """Independent numpy restatement of ct_ss_mats (SolverMPC.cpp:260-279), float64."""
-    q = rec[6:10].astype(np.float64)
-    w_, x, y, z = q
-    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w_ * z), 2 * (x * z + w_ * y)],
-                  [2 * (x * y + w_ * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w_ * x)],
-                  [2 * (x * z - w_ * y), 2 * (y * z + w_ * x), 1 - 2 * (x * x + y * y)]])
-    Iw = R @ np.diag([.07, .26, .242]) @ R.T
-    Ii = np.linalg.inv(Iw)
-    r = rec[13:25].reshape(3, 4).astype(np.float64)
-    A = np.zeros((13, 13)); B = np.zeros((13, 12))
-    A[3, 9] = A[4, 10] = A[5, 11] = A[11, 12] = 1.0
-    A[11, 9] = rec[28]
-    A[0:3, 6:9] = R.T
-    for b in range(4):
-        rx = np.array([[0, -r[2, b], r[1, b]], [r[2, b], 0, -r[0, b]], [-r[1, b], r[0, b], 0]])
-        B[6:9, 3 * b:3 * b + 3] = Ii @ rx
-        B[9:12, 3 * b:3 * b + 3] = np.eye(3) / 12.0
-    Q = np.zeros((13, 6)); Q[6:12] = np.eye(6)
-    return A, B, Q
-
-
 def test_discretisation_matches_expm(cm, orc):
     prm = cm.make_params(10)
     recs = cm.make_instances(16, 10, seed=5)
     for rec in recs:
         c = orc.condense(rec, prm, full=False)
-        A, B, Q = _ct_mats(rec)
+        A, B, Q = orc.ct_mats64(rec)
         M = np.zeros((31, 31))
         M[:13, :13] = A; M[:13, 13:25] = B; M[:13, 25:31] = Q
         E = expm(prm.dt * M)
@@ -44,10 +22,10 @@ def test_discretisation_matches_expm(cm, orc):
         np.testing.assert_allclose(c["Qdt"], E[:13, 25:31], rtol=0, atol=2e-7)
 
 
-def test_nilpotent_generator(cm):
+def test_nilpotent_generator(cm, orc):
     """A_c^3 = 0 for every state (the closed-form discretisation relies on it)."""
     for rec in cm.make_instances(8, 10, seed=6):
-        A, _, _ = _ct_mats(rec)
+        A, _, _ = orc.ct_mats64(rec)
         assert np.abs(np.linalg.matrix_power(A, 3)).max() == 0.0
 
 
@@ -205,3 +183,19 @@ def test_config5_golden_self_consistent(cm, orc):
         st = np.zeros(orc.EST_WORDS, np.float32)
         seq = [orc.est_step(st, g["f3"][i, k], g["t"][k])[0] for k in range(g["f3"].shape[1])]
         np.testing.assert_array_equal(np.array(seq, np.float32), g["fest_ref"][i])
+
+
+def test_fp64_pipeline_close_to_reference(cm, orc):
+    """oracle.fp64_solve (the float64 optimum the parity rule at N >= 16 falls back to) agrees
+    with the reference fp32 pipeline to the reference's own rounding: <= 2e-5 at N = 10 and
+    <= 1.5e-4 at N = 20 (scripts/exact_gap.py)."""
+    if not orc.ref_available():
+        pytest.skip("oracle/_ref not present")
+    for N, tol in ((10, 2e-5), (20, 1.5e-4)):
+        prm = cm.make_params(N)
+        recs = cm.make_instances(8, N, seed=4242 + N, random_contact_frac=0.5)
+        q, st, _ = orc.ref_solve_batch(recs, prm, nthreads=4)
+        for i in range(len(recs)):
+            x64, ri = orc.fp64_solve(recs[i], prm)
+            assert ri == 0 and st[i] == 0
+            assert np.abs(q[i] - x64).max() / max(np.abs(x64).max(), 1.0) <= tol
