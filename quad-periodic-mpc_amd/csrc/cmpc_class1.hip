@@ -73,7 +73,7 @@ struct SharedC1 {
   float ibuf[NV];          // 1 / sqrt(d_k) of pivot k
   float gbuf[NV];          // gradient border of pivot k
   float vbuf[NV];          // broadcast vector (y, then masked d)
-  float bufA[NV], bufB[NV];  // published J rows ia, iz
+  float bufA[NV], bufB[NV];  // published J rows ia, iz (contiguous: bufA[NV + c] = bufB[c])
   float xs[NV];
   float cs[2 * NV];        // Givens (c, s) per column pair
   float sub[4 * MAXN];     // ub of each stance foot-step (gait * f_max)
@@ -273,28 +273,46 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   lsync();
 
   // ---- bordered Cholesky [H | g]: raw column k = slot[k] of every lane -> P row k ----------
+  // Look-ahead: step k publishes column k+1 (and reads its pivot d_{k+1}) as soon as the sweep
+  // chunk holding slot[k+1] is updated, so the LDS store -> load round trip of the next pivot
+  // overlaps the rest of step k's sweep instead of heading step k+1.
   int status = CMPC_OK;
   float my_inv = 1.f;
+  float dnext = 1.f;
+  if (n > 0) {
+    sh.P[prow(0) + v] = slot[0];
+    if (v == 0) sh.gbuf[0] = slot[NV];
+    lsync();
+    dnext = sh.P[prow(0)];
+  }
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int c0 = k & ~3;
     constexpr int rk = prow(k);
+    constexpr int k1 = k + 1;
+    constexpr int c1 = k1 & ~3;
     if (k < n) {
-      if (v >= c0) sh.P[rk + v - c0] = (v >= k) ? slot[k] : 0.f;
-      if (v == k) sh.gbuf[k] = slot[NV];
-      lsync();
-      float d = sh.P[rk + k - c0];
+      float d = dnext;
       if (!(d > 0.f)) { status = CMPC_NOT_PD; d = 1e-30f; }
       const float inv = rsqrtf(d);
       if (v == k) { my_inv = inv; sh.ibuf[k] = inv; }
       const float a = (v > k) ? -slot[k] * (inv * inv) : 0.f;
+      slot[NV] = fmaf(a, sh.gbuf[k], slot[NV]);
 #pragma unroll
       for (int c = c0; c < NV; c += 4) {
         const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
         axpy4(a, r4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
+        if constexpr (k1 < NV) {
+          if (c == c1 && k1 < n) {  // publish column k+1 (final after this chunk)
+            constexpr int rk1 = prow(k1);
+            if (v >= c1) sh.P[rk1 + v - c1] = (v >= k1) ? slot[k1] : 0.f;
+            if (v == k1) sh.gbuf[k1] = slot[NV];
+            lsync();
+            dnext = sh.P[rk1 + k1 - c1];
+          }
+        }
         CMPC_SWEEP_FENCE(c);
       }
-      slot[NV] = fmaf(a, sh.gbuf[k], slot[NV]);
       pin(slot);
     }
   });
@@ -311,8 +329,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     constexpr int k = decltype(KC)::value;
     constexpr int c0 = k & ~3;
     constexpr int rk = prow(k);
-    if (k < n) {
-      lsync();
+    if (k < n) {  // P and ibuf are read-only here: no per-step LDS ordering needed
       const float inv = sh.ibuf[k];
       const float xk = slot[k] * inv;
       const float a = -xk * inv;
@@ -391,13 +408,13 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
       // d = J' n+ : rows ia, iz of J through LDS (dword stores: wide stores would tie the row
       // registers into tuples)
-      if (v == cp.ia && cp.ia != cp.iz) {
+      if (v == cp.ia || v == cp.iz) {  // both rows in one pass (two lanes per store)
+        const int boff = (v == cp.iz) ? NV : 0;  // bufB follows bufA
 #pragma unroll
-        for (int c = 0; c < NV; c++) sh.bufA[c] = slot[c];
-      }
-      if (v == cp.iz) {
-#pragma unroll
-        for (int c = 0; c < NV; c++) sh.bufB[c] = slot[c];
+        for (int c = 0; c < NV; c++) {
+          sh.bufA[boff + c] = slot[c];
+          if ((c & 15) == 15) __builtin_amdgcn_sched_barrier(0);
+        }
       }
       lsync();
       const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[v], cp.cb * sh.bufB[v]) : cp.cb * sh.bufB[v];
@@ -493,8 +510,10 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         }
       }
       lsync();
-      // J <- J (I - beta w w'): tw = J_v . w, J_v -= beta tw w  (no-op on a drop: beta = 0)
+      // Both J updates run as straight-line code on every trip (a uniform add/drop branch here
+      // makes the allocator duplicate the row: 224-256 VGPRs instead of 166).
       {
+        // J <- J (I - beta w w'): tw = J_v . w, J_v -= beta tw w  (no-op on a drop: beta = 0)
         f2v tacc = {0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < NV; c += 4) {
@@ -513,15 +532,17 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           CMPC_SWEEP_FENCE(c);
         }
       }
-      // J columns (j, j+1) <- Givens chain j = 0 .. NV-2 (identity on an add)
-      static_for<0, NV - 1>([&](auto JC) {
-        constexpr int j = decltype(JC)::value;
-        const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
-        const float x0 = slot[j], x1 = slot[j + 1];
-        slot[j] = fmaf(cs2.x, x0, cs2.y * x1);
-        slot[j + 1] = fmaf(-cs2.y, x0, cs2.x * x1);
-        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-      });
+      {
+        // J columns (j, j+1) <- Givens chain j = 0 .. NV-2 (identity on an add)
+        static_for<0, NV - 1>([&](auto JC) {
+          constexpr int j = decltype(JC)::value;
+          const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+          const float x0 = slot[j], x1 = slot[j + 1];
+          slot[j] = fmaf(cs2.x, x0, cs2.y * x1);
+          slot[j + 1] = fmaf(-cs2.y, x0, cs2.x * x1);
+          if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        });
+      }
       if (add) {
         q++;
         p = -1;

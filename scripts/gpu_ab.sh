@@ -10,5 +10,5 @@ i=0
 for kv in "$@"; do
   i=$((i + 1))
   env $kv timeout -k 10 120 python3 -u bench.py --no-cpu-baseline > gpurun_out/ab/bench_$i.log 2>&1 || exit 1
-  python3 -c "import json; d=json.loads(open('gpurun_out/ab/bench_$i.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$kv', d['value'], d['ms_per_step'], r['avg_launch_ms'], r['class2_avg_launch_ms'])"
+  python3 -c "import json; d=json.loads(open('gpurun_out/ab/bench_$i.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$kv', d['value'], d['ms_per_step'], r['avg_launch_ms'], r.get('tail_avg_ms'))"
 done
