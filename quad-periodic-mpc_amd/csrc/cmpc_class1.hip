@@ -27,6 +27,11 @@
 #ifndef CMPC_W1_WAVES_PER_EU
 #define CMPC_W1_WAVES_PER_EU 2
 #endif
+// Cholesky sweep chunks (of every 4) whose column broadcast goes through v_readlane instead of
+// the LDS (see the Cholesky stage)
+#ifndef CMPC_C1_RL
+#define CMPC_C1_RL 0
+#endif
 
 // Phase profiler (diagnostic builds only, -DCMPC_PHASE_PROF): lane 0 of every solved instance
 // adds the s_memtime cycles spent in each stage to g_c1_phase (scripts/phase_prof.py).
@@ -71,7 +76,6 @@ struct SharedC1 {
   float P[PSZ];
   float BdtT[12][16];
   float ibuf[NV];          // 1 / sqrt(d_k) of pivot k
-  float gbuf[NV];          // gradient border of pivot k
   float vbuf[NV];          // broadcast vector (y, then masked d)
   float bufA[NV], bufB[NV];  // published J rows ia, iz (contiguous: bufA[NV + c] = bufB[c])
   float xs[NV];
@@ -105,9 +109,12 @@ __device__ __forceinline__ void pin(float (&x)[M]) {
 
 // Scheduling fence inside long unrolled LDS->FMA sweeps: without it the scheduler issues every
 // ds_read_b128 of a row up front (64 extra live VGPRs on top of the 65-slot row).
-#define CMPC_SWEEP_FENCE(c)                                  \
-  do {                                                       \
-    if (((c) & 15) == 12) __builtin_amdgcn_sched_barrier(0); \
+#ifndef CMPC_FENCE_COLS
+#define CMPC_FENCE_COLS 16
+#endif
+#define CMPC_SWEEP_FENCE(c)                                                                  \
+  do {                                                                                       \
+    if (((c) & (CMPC_FENCE_COLS - 1)) == CMPC_FENCE_COLS - 4) __builtin_amdgcn_sched_barrier(0); \
   } while (0)
 
 __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KParams& P,
@@ -273,17 +280,21 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   lsync();
 
   // ---- bordered Cholesky [H | g]: raw column k = slot[k] of every lane -> P row k ----------
-  // Look-ahead: step k publishes column k+1 (and reads its pivot d_{k+1}) as soon as the sweep
-  // chunk holding slot[k+1] is updated, so the LDS store -> load round trip of the next pivot
-  // overlaps the rest of step k's sweep instead of heading step k+1.
+  // Look-ahead: step k publishes column k+1 (and takes its pivot d_{k+1} and border g_{k+1})
+  // as soon as the sweep chunk holding slot[k+1] is updated, so nothing of step k+1's setup
+  // waits on the LDS. The broadcast of column k to every lane is split between two paths that
+  // run concurrently: CMPC_C1_RL of every 4 sweep chunks take it by v_readlane into SGPRs (FMA
+  // with an SGPR operand, VALU only), the others by ds_read_b128 broadcasts of the stored
+  // column (the LDS delivers 4 B per lane per cycle; with every chunk on it the sweep is LDS
+  // bound). The stored columns also feed J = L^-T below.
   int status = CMPC_OK;
   float my_inv = 1.f;
-  float dnext = 1.f;
+  float dnext = 1.f, gnext = 0.f;
   if (n > 0) {
     sh.P[prow(0) + v] = slot[0];
-    if (v == 0) sh.gbuf[0] = slot[NV];
+    dnext = rl(slot[0], 0);
+    gnext = rl(slot[NV], 0);
     lsync();
-    dnext = sh.P[prow(0)];
   }
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
@@ -293,26 +304,43 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     constexpr int c1 = k1 & ~3;
     if (k < n) {
       float d = dnext;
+      const float gk = gnext;
       if (!(d > 0.f)) { status = CMPC_NOT_PD; d = 1e-30f; }
-      const float inv = rsqrtf(d);
+      const float inv = __builtin_amdgcn_rsqf(d);  // d is a normal positive pivot
       if (v == k) { my_inv = inv; sh.ibuf[k] = inv; }
-      const float a = (v > k) ? -slot[k] * (inv * inv) : 0.f;
-      slot[NV] = fmaf(a, sh.gbuf[k], slot[NV]);
-#pragma unroll
-      for (int c = c0; c < NV; c += 4) {
-        const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
-        axpy4(a, r4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
-        if constexpr (k1 < NV) {
-          if (c == c1 && k1 < n) {  // publish column k+1 (final after this chunk)
+      const float colk = slot[k];  // lane c holds the raw column entry of row c
+      const float a = (v > k) ? -colk * (inv * inv) : 0.f;
+      slot[NV] = fmaf(a, gk, slot[NV]);
+      static_for<c0 / 4, NV / 4>([&](auto JC) {
+        constexpr int c = 4 * decltype(JC)::value;
+        if constexpr (((c / 4) & 3) < CMPC_C1_RL) {
+          // four readlanes into distinct SGPRs ahead of the four FMAs: a readlane's SGPR
+          // result needs two wait states before a VALU may read it
+          float s4[4];
+          static_for<0, 4>([&](auto EC) {
+            constexpr int cc = c + decltype(EC)::value;
+            s4[EC] = (cc >= k) ? rl(colk, cc) : 0.f;
+          });
+          asm volatile("" : "+s"(s4[0]), "+s"(s4[1]), "+s"(s4[2]), "+s"(s4[3]));
+          static_for<0, 4>([&](auto EC) {
+            constexpr int cc = c + decltype(EC)::value;
+            if constexpr (cc >= k) slot[cc] = fmaf(a, s4[EC], slot[cc]);
+          });
+        } else {
+          const float4 r4 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
+          axpy4(a, r4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
+        }
+        if constexpr (k1 < NV && c == c1) {
+          if (k1 < n) {  // publish column k+1 (final after this chunk)
             constexpr int rk1 = prow(k1);
             if (v >= c1) sh.P[rk1 + v - c1] = (v >= k1) ? slot[k1] : 0.f;
-            if (v == k1) sh.gbuf[k1] = slot[NV];
+            dnext = rl(slot[k1], k1);
+            gnext = rl(slot[NV], k1);
             lsync();
-            dnext = sh.P[rk1 + k1 - c1];
           }
         }
         CMPC_SWEEP_FENCE(c);
-      }
+      });
       pin(slot);
     }
   });

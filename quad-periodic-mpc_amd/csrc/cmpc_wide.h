@@ -345,7 +345,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       wbar();
       float d = sh.P[base + kh * st + kj - j0];
       if (!(d > 0.f)) { status = CMPC_NOT_PD; d = 1e-30f; }
-      const float inv = rsqrtf(d);
+      const float inv = __builtin_amdgcn_rsqf(d);  // raw v_rsq: d is a normal positive pivot
       if (r == k) { my_inv = inv; if (h == 0) sh.ibuf[k] = inv; }
       const float a = (r > k && r < NV) ? -hrk * (inv * inv) : 0.f;
       const float* prow = &sh.P[base + h * st - j0];

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lib", default=PROF_LIB)
     a = ap.parse_args()
     if a.build:
         b = importlib.import_module("quad-periodic-mpc_amd.build")
@@ -38,7 +39,7 @@ def main():
     import torch
 
     solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
-    lib = solver_mod.load_library(PROF_LIB)
+    lib = solver_mod.load_library(a.lib)
     cm = importlib.import_module("quad-periodic-mpc_amd")
     N, B = a.horizon, a.batch
     recs = torch.from_numpy(cm.make_instances(B, N)).cuda()
