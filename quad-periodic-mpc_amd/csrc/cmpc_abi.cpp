@@ -47,6 +47,11 @@ struct cmpc_batch {
   float* d_forces = nullptr;
   uint8_t* d_status = nullptr;
   int32_t* d_iters = nullptr;
+  // single-instance fast path of cmpc_batch_solve_host: the one-entry instance list {1, 0}, the
+  // instance's forces + status word (one D2H), pinned host staging of record and result
+  int* d_one = nullptr;
+  float* d_single_out = nullptr;
+  float* h_pin = nullptr;
   // side streams + fork/join events for the wider size classes (cmpc_launch.hip)
   cmpc::LaunchCtx ctx;
   // optional per-launch timing (cmpc_batch_enable_timing)
@@ -186,6 +191,9 @@ extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (h->d_forces) (void)hipFree(h->d_forces);
   if (h->d_status) (void)hipFree(h->d_status);
   if (h->d_iters) (void)hipFree(h->d_iters);
+  if (h->d_one) (void)hipFree(h->d_one);
+  if (h->d_single_out) (void)hipFree(h->d_single_out);
+  if (h->h_pin) (void)hipHostFree(h->h_pin);
   for (auto e : h->ev) (void)hipEventDestroy(e);
   for (int j = 0; j < cmpc::kSideStreams; j++) {
     if (h->ctx.side[j]) (void)hipStreamDestroy(h->ctx.side[j]);
@@ -327,6 +335,53 @@ static int ensure_staging(cmpc_batch* h) {
   // qH / qg of one instance at the largest horizon (the single-instance ADMM path)
   const size_t nv = 12 * (size_t)CMPC_MAX_HORIZON;
   if ((e = hipMalloc(&h->d_admm_H, (nv * nv + nv) * sizeof(float))) != hipSuccess) return fail("hipMalloc", e);
+  const int one[2] = {1, 0};
+  if ((e = hipMalloc(&h->d_one, sizeof(one))) != hipSuccess) return fail("hipMalloc", e);
+  if ((e = hipMemcpy(h->d_one, one, sizeof(one), hipMemcpyHostToDevice)) != hipSuccess) return fail("H2D", e);
+  if ((e = hipMalloc(&h->d_single_out, (12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) != hipSuccess)
+    return fail("hipMalloc", e);
+  if ((e = hipHostMalloc(reinterpret_cast<void**>(&h->h_pin),
+                         (CMPC_REC_WORDS(CMPC_MAX_HORIZON) + 12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) != hipSuccess)
+    return fail("hipHostMalloc", e);
+  return 0;
+}
+
+// reduced size n = 3 x (stance foot-steps) of one record: eliminated iff |gait * f_max| < 0.01,
+// the test of the classify pass and of every solver kernel (SolverMPC.cpp:869-894)
+static int host_reduced_size(const float* rec, int N, float f_max) {
+  const unsigned char* gait = reinterpret_cast<const unsigned char*>(rec + CMPC_REC_GAIT(N));
+  int nfs = 0;
+  for (int t = 0; t < 4 * N; t++) {
+    const float ub = (float)gait[t] * f_max;
+    nfs += (ub < 0.01f && ub > -0.01f) ? 0 : 1;
+  }
+  return 3 * nfs;
+}
+
+// batch == 1 from host memory: one kernel of the instance's class, pinned copies, one D2H
+static int solve_single_host(cmpc_batch* h, const float* record, float* forces, uint8_t* status,
+                             int32_t* iters) {
+  const int N = h->prm.horizon;
+  const size_t rw = (size_t)CMPC_REC_WORDS(N);
+  const int n = host_reduced_size(record, N, h->prm.f_max);
+  float* pin_rec = h->h_pin;
+  float* pin_out = h->h_pin + CMPC_REC_WORDS(CMPC_MAX_HORIZON);
+  std::memcpy(pin_rec, record, rw * sizeof(float));
+  float* d_out = h->d_single_out;
+  uint8_t* d_st = reinterpret_cast<uint8_t*>(d_out + 12 * N);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(h->d_rec, pin_rec, rw * sizeof(float), hipMemcpyHostToDevice, h->stream)) != hipSuccess)
+    return fail("H2D", e);
+  if ((e = cmpc::launch_single(h->d_rec, n, h->kp, d_out, d_st, h->d_iters, h->d_one, h->d_gscratch,
+                               h->stream)) != hipSuccess)
+    return fail("launch_single", e);
+  if ((e = hipMemcpyAsync(pin_out, d_out, (12 * N + 1) * sizeof(float), hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+    return fail("D2H", e);
+  if (iters && (e = hipMemcpyAsync(iters, h->d_iters, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+    return fail("D2H", e);
+  if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail("sync", e);
+  std::memcpy(forces, pin_out, 12 * N * sizeof(float));
+  if (status) std::memcpy(status, pin_out + 12 * N, 1);
   return 0;
 }
 
@@ -337,6 +392,10 @@ extern "C" int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int ba
   if (int r = ensure_staging(h)) return r;
   const int N = h->prm.horizon;
   const size_t rw = (size_t)CMPC_REC_WORDS(N);
+  // one instance (the reference ABI's operating mode): the fast path, unless per-launch timing
+  // is on (it brackets the batched launch sequence) or the instance needs class G's slabs
+  if (batch == 1 && h->ev_steps == 0 && host_reduced_size(records, N, h->prm.f_max) <= 256)
+    return solve_single_host(h, records, forces, status, iters);
   hipError_t e;
   if ((e = hipMemcpyAsync(h->d_rec, records, rw * batch * sizeof(float), hipMemcpyHostToDevice, h->stream)) != hipSuccess)
     return fail("H2D", e);
@@ -411,21 +470,50 @@ std::vector<double> gaussian_filter(const std::vector<double>& data, float sigma
   return out;
 }
 
+// Mixed-radix decimation-in-time DFT, in place (the reference calls FFTW's r2c here): data[0..n)
+// with twiddles tw[j] = exp(-2 pi i j / N) of the top-level size N, stride_tw = N / n, and a
+// scratch of n. Prime factors beyond the smallest split are done directly.
+void fft_mixed(std::complex<double>* data, int n, int stride_tw, const std::vector<std::complex<double>>& tw,
+               std::complex<double>* scratch) {
+  if (n == 1) return;
+  const int N = (int)tw.size();
+  int p = 2;
+  while (n % p) p++;
+  if (p == n) {  // prime length: direct
+    for (int k = 0; k < n; k++) {
+      std::complex<double> acc(0, 0);
+      for (int t = 0; t < n; t++) acc += data[t] * tw[((long)stride_tw * k * t) % N];
+      scratch[k] = acc;
+    }
+    for (int k = 0; k < n; k++) data[k] = scratch[k];
+    return;
+  }
+  const int m = n / p;
+  for (int r = 0; r < p; r++)
+    for (int j = 0; j < m; j++) scratch[r * m + j] = data[j * p + r];
+  for (int r = 0; r < p; r++) fft_mixed(scratch + r * m, m, stride_tw * p, tw, data + r * m);
+  for (int k = 0; k < m; k++)
+    for (int q = 0; q < p; q++) {
+      std::complex<double> acc(0, 0);
+      for (int r = 0; r < p; r++) acc += scratch[r * m + k] * tw[((long)stride_tw * r * (k + q * m)) % N];
+      data[k + q * m] = acc;
+    }
+}
+
 // fit_sin initial guesses (SolverMPC.cpp:478-541): peak |rfft| bin >= 1, amp = sqrt2 std,
-// offset = mean, phase = 0. The r2c magnitudes are evaluated by a direct DFT (W = 400 bins).
+// offset = mean, phase = 0. The r2c magnitudes come from a mixed-radix FFT (400 = 2^4 5^2).
 void fit_sin(const std::vector<double>& tt, const std::vector<double>& yy, double& amp,
              double& freq, double& phase, double& offset) {
   const int n = (int)tt.size();
   const double dt = tt[1] - tt[0];
+  std::vector<std::complex<double>> tw(n), X(n), scratch(n);
+  for (int j = 0; j < n; j++) tw[j] = std::polar(1.0, -2.0 * M_PI * (double)j / (double)n);
+  for (int t = 0; t < n; t++) X[t] = std::complex<double>(yy[t], 0.0);
+  fft_mixed(X.data(), n, 1, tw, scratch.data());
   int best = 1;
   double best_mag = -1.0;
   for (int k = 1; k <= n / 2; k++) {
-    std::complex<double> acc(0, 0);
-    for (int t = 0; t < n; t++) {
-      const double ang = -2.0 * M_PI * (double)k * (double)t / (double)n;
-      acc += yy[t] * std::complex<double>(std::cos(ang), std::sin(ang));
-    }
-    const double mag = std::abs(acc);
+    const double mag = std::abs(X[k]);
     if (k == 1 || mag > best_mag) { best_mag = mag; best = k; }
   }
   const double f = (best <= n / 2) ? best / (n * dt) : (best - n) / (n * dt);

@@ -80,6 +80,9 @@ CMPC_DECL_WIDE(128)
 CMPC_DECL_WIDE(192)
 CMPC_DECL_WIDE(256)
 #undef CMPC_DECL_WIDE
+hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_forces,
+                         uint8_t* d_status, int32_t* d_iters, const int* d_one, float* d_gscratch,
+                         hipStream_t stream);
 hipError_t launch_classg(const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          float* scratch, int grid, hipStream_t stream);

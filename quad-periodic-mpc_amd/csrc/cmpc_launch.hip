@@ -153,4 +153,23 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   return hipSuccess;
 }
 
+// One instance whose reduced size n the caller already knows (counted on the host from the
+// record's gait table, the same test as the classify pass): exactly one kernel of the right
+// class, no classify pass, no side-stream fork/join. d_one = {1, 0}: a one-entry instance list.
+hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_forces,
+                         uint8_t* d_status, int32_t* d_iters, const int* d_one, float* d_gscratch,
+                         hipStream_t stream) {
+  const int* cnt = d_one;
+  const int* lst = d_one + 1;
+  if (n <= 64)
+    return launch_class1(d_rec, 1, P, d_forces, d_status, d_iters, nullptr, nullptr, nullptr, nullptr,
+                         1, stream);
+  if (n <= 80) return launch_wide_w80(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
+  if (n <= 96) return launch_wide_w96(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
+  if (n <= 128) return launch_wide_w128(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
+  if (n <= 192) return launch_wide_w192(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
+  if (n <= 256) return launch_wide_w256(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
+  return launch_classg(d_rec, 1, P, d_forces, d_status, d_iters, lst, cnt, d_gscratch, 1, stream);
+}
+
 }  // namespace cmpc

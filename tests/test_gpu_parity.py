@@ -170,3 +170,21 @@ def test_reference_call_protocol(cm, orc, solver_mod):
                                               rec[32:32 + 12 * N], prm.alpha, gait)
         sol = np.array([solver_mod.get_solution(j) for j in range(12 * N)])
         assert rel_force_err(sol[None], g["q_ref"][i][None]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("N,frac", [(10, 0.5), (20, 1.0)])
+def test_single_instance_fast_path_bitwise(cm, solver_mod, N, frac):
+    """batch == 1 from host memory takes the one-kernel fast path (host-counted size class, no
+    classify pass); it must reproduce the batched launch bit for bit, in every size class
+    (N = 10 with random contacts: class 1 and wide 80/96; N = 20: wide 128/192/256)."""
+    prm = cm.make_params(N)
+    recs = cm.make_instances(48, N, seed=900 + N, random_contact_frac=frac)
+    f_b, st_b, it_b = gpu_solve(solver_mod, prm, recs)
+    s = solver_mod.BatchSolver(prm, max_batch=1)
+    try:
+        for i in range(len(recs)):
+            f1, st1, it1 = s.solve_host(recs[i:i + 1])
+            assert st1[0] == st_b[i] and it1[0] == it_b[i]
+            np.testing.assert_array_equal(f1[0], f_b[i])
+    finally:
+        s.close()
