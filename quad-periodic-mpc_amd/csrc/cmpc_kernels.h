@@ -33,7 +33,7 @@ struct LocoParams {
 // Scratch ints needed by launch_solve for max_batch instances.
 // d_work: [0] instances with n > 64, [1..6] lengths of the class lists (wide classes of 80, 96,
 // 128, 192, 256 columns, general), [8 ..) the six lists of max_batch entries each
-constexpr int kLists = 6;
+constexpr int kLists = 7;  // 80, 96, 128, 192, 256, G, 144 (cnt[1 + list])
 inline size_t work_ints(int max_batch) { return 8 + kLists * (size_t)max_batch; }
 // Side streams and events of one handle: the wider size classes run concurrently with class 1
 // (they are latency-bound: few instances, long serial solves). Two side streams: with the
@@ -69,7 +69,7 @@ CMPC_DECL_CLASS2(80)
 CMPC_DECL_CLASS2(96)
 CMPC_DECL_CLASS2(128)
 #undef CMPC_DECL_CLASS2
-// wide classes, two lanes per row, NV/32 wavefronts (cmpc_wide_w{80,96,128,192,256}.hip)
+// wide classes, two lanes per row, NV/32 wavefronts (cmpc_wide_w{80,96,128,144,192,256}.hip)
 #define CMPC_DECL_WIDE(W)                                                                          \
   hipError_t launch_wide_w##W(const float* d_recs, const KParams& P, float* d_forces,             \
                               uint8_t* d_status, int32_t* d_iters, const int* in_list,            \
@@ -77,6 +77,7 @@ CMPC_DECL_CLASS2(128)
 CMPC_DECL_WIDE(80)
 CMPC_DECL_WIDE(96)
 CMPC_DECL_WIDE(128)
+CMPC_DECL_WIDE(144)
 CMPC_DECL_WIDE(192)
 CMPC_DECL_WIDE(256)
 #undef CMPC_DECL_WIDE

@@ -41,8 +41,8 @@ __global__ __launch_bounds__(256) void cmpc_classify_kernel(const float* __restr
 #ifdef CMPC_LEGACY_C2
     cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : 5;
 #else
-    cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : (n <= 192) ? 3
-        : (n <= 256) ? 4 : 5;
+    cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : (n <= 144) ? 6
+        : (n <= 192) ? 3 : (n <= 256) ? 4 : 5;
 #endif
   }
   const unsigned long long any = __ballot(cls >= 0);
@@ -84,11 +84,12 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
     for (int s = 0; s < kSideStreams; s++)
       if ((e = hipStreamWaitEvent(ctx.side[s], ctx.fork, 0)) != hipSuccess) return e;
-    // one workgroup per possible list entry (the lengths are only known on the device);
-    // surplus workgroups exit after one load. CMPC_EXACT_GRID=1 (diagnostic): read the list
-    // lengths back first (a host round trip per solve) and launch exact grids
     int grid_of[kLists];
     for (int j = 0; j < kLists; j++) grid_of[j] = batch;
+    // one workgroup per possible list entry (the lengths are only known on the device);
+    // surplus workgroups exit after one load. CMPC_EXACT_GRID=1 (diagnostic): read the list
+    // lengths back first (a host round trip per solve) and launch exact grids. Measured: +1 % at
+    // config 3, +0.2 % at config 5 (where the 256-row class launches only empty workgroups)
     static const bool exact = [] {
       const char* v = getenv("CMPC_EXACT_GRID");
       return v && v[0] == '1';
@@ -114,8 +115,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       return e;
     const bool g_possible = n_max > 128;
 #else
-    // side 0: 80, 128, 256; side 1: 96, 192 (at N = 20 the 128- and 192-column classes, which
-    // carry the batch, run side by side)
+    // side 0: 80, 128, 256; side 1: 96, 144, 192 (at N = 20 the 128-column class and the
+    // 144/192-column classes, which carry the batch, run side by side)
     if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], grid_of[0],
                              ctx.side[0])) != hipSuccess)
       return e;
@@ -125,7 +126,11 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if (n_max > 96 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
                                             grid_of[2], ctx.side[0])) != hipSuccess)
       return e;
-    if (n_max > 128 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4],
+    if (n_max > 128 &&
+        (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], grid_of[6],
+                              ctx.side[1])) != hipSuccess)
+      return e;
+    if (n_max > 144 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4],
                                              grid_of[3], ctx.side[1])) != hipSuccess)
       return e;
     if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5],
@@ -167,6 +172,7 @@ hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_f
   if (n <= 80) return launch_wide_w80(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
   if (n <= 96) return launch_wide_w96(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
   if (n <= 128) return launch_wide_w128(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
+  if (n <= 144) return launch_wide_w144(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
   if (n <= 192) return launch_wide_w192(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
   if (n <= 256) return launch_wide_w256(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
   return launch_classg(d_rec, 1, P, d_forces, d_status, d_iters, lst, cnt, d_gscratch, 1, stream);

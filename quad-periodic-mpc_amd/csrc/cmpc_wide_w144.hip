@@ -1,0 +1,16 @@
+// cmpc_wide_w144.hip — wide size class with 144-column rows (n 129-144: random contact tables at N = 20) (kernel template: cmpc_wide.h).
+// two waves per SIMD: at three the 72-column half rows spill (25 VGPRs); five waves per
+// workgroup, 52 KB of LDS
+#define CMPC_WIDE_WAVES_PER_EU 2
+#include "cmpc_wide.h"
+
+namespace cmpc {
+
+hipError_t launch_wide_w144(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
+                          int32_t* d_iters, const int* in_list, const int* in_count, int grid,
+                          hipStream_t stream) {
+  return launch_wide_impl<144>(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, grid,
+                              stream);
+}
+
+}  // namespace cmpc

@@ -17,7 +17,7 @@ PASS_sq1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WA
 PASS_sq2="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 for c in $CASES; do
   case $c in
-    cfg3) args="" ;;
+    cfg3) args="--config 3" ;;
     cfg5) args="--config 5" ;;
     n16) args="--horizon 16 --random-contact-frac 0" ;;
     *) echo "unknown case $c"; exit 1 ;;
