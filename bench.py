@@ -285,7 +285,7 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
         "unit": "TFLOP/s",
         "frac": round(achieved / FP32_PEAK_TFLOPS, 5) if achieved else None,
         "traffic": traffic,
-        "kernel": ("cmpc_solve_c1_kernel (n <= 64 class, one wavefront per instance)" if not wide
+        "kernel": ("cmpc_solve_c1_kernel<60> (n <= 60 class: 60-wide rows, one wavefront per instance)" if not wide
                    else "whole solve: every size class, concurrent streams"),
         "units_per_launch": int(units1),
         "flops_per_unit": fl,

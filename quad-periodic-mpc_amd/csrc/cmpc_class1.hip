@@ -52,40 +52,48 @@ __device__ unsigned long long g_c1_phase[8];
 namespace cmpc {
 namespace {
 
-constexpr int NV = 64;
-constexpr int NG = NV / 4;
-constexpr int PSZ = 4 * NG * NV - 8 * NG * (NG - 1);  // packed rows r: columns [r & ~3, NV)
+constexpr int NL = 64;  // lanes of the wavefront (per-lane LDS arrays are sized by it)
 
-// offset of packed row r (16-B aligned)
-__host__ __device__ constexpr int prow(int r) {
-  return 4 * (r >> 2) * NV - 8 * (r >> 2) * ((r >> 2) - 1) + (r & 3) * (NV - 4 * (r >> 2));
-}
-// prow(r) - (r & ~3): element (r, c) lives at prow0(r) + c
-__host__ __device__ constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+// Row width NV (60 or 64: the 60-wide build takes every instance with n <= 60, i.e. all trot
+// instances at N = 10, and saves the padding columns of the 64-wide sweeps); lanes v >= NV of a
+// 60-wide build own no row.
+template <int NV>
+struct C1Geo {
+  static constexpr int NG = NV / 4;
+  static constexpr int PSZ = 4 * NG * NV - 8 * NG * (NG - 1);  // packed rows r: columns [r & ~3, NV)
+  // offset of packed row r (16-B aligned)
+  __host__ __device__ static constexpr int prow(int r) {
+    return 4 * (r >> 2) * NV - 8 * (r >> 2) * ((r >> 2) - 1) + (r & 3) * (NV - 4 * (r >> 2));
+  }
+  // prow(r) - (r & ~3): element (r, c) lives at prow0(r) + c
+  __host__ __device__ static constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+};
 // R (upper triangular, q x q) packed by columns: R[i][j] at rcol(j) + i, i <= j
 __device__ __forceinline__ int rcol(int j) { return (j * (j + 1)) >> 1; }
-static_assert(NV * (NV + 1) / 2 <= PSZ, "R must fit in P");
 
 // prep scratch inside P (P is not yet holding H while these are live)
 constexpr int OFF_E = 0;
 constexpr int OFF_ZE = OFF_E + 16 * MAXN;
 constexpr int OFF_REC = OFF_ZE + 16 * MAXN;  // LDS copy of the instance record (16-B aligned)
-static_assert(OFF_REC + CMPC_REC_WORDS(MAXN) <= PSZ, "prep scratch must fit in P");
 
+template <int NV>
 struct SharedC1 {
-  float P[PSZ];
+  static_assert(NV % 4 == 0 && NV <= NL, "row width");
+  static_assert(NV * (NV + 1) / 2 <= C1Geo<NV>::PSZ, "R must fit in P");
+  static_assert(OFF_REC + CMPC_REC_WORDS(MAXN) <= C1Geo<NV>::PSZ, "prep scratch must fit in P");
+  float P[C1Geo<NV>::PSZ];
   float BdtT[12][16];
-  float ibuf[NV];          // 1 / sqrt(d_k) of pivot k
-  float vbuf[NV];          // broadcast vector (y, then masked d)
-  float bufA[NV], bufB[NV];  // published J rows ia, iz (contiguous: bufA[NV + c] = bufB[c])
-  float xs[NV];
-  float cs[2 * NV];        // Givens (c, s) per column pair
+  float ibuf[NL];          // 1 / sqrt(d_k) of pivot k
+  float vbuf[NL];          // broadcast vector (y, then masked d)
+  float bufA[NL], bufB[NL];  // published J rows ia, iz (contiguous: bufA[NL + c] = bufB[c])
+  float xs[NL];
+  float cs[2 * NL];        // Givens (c, s) per column pair
   float sub[4 * MAXN];     // ub of each stance foot-step (gait * f_max)
   int sfs[4 * MAXN];       // stance foot-step ids, in order
   int blkbase[MAXN + 2];   // first reduced variable of each horizon step
-  unsigned char varblk[NV], varcol[NV];
+  unsigned char varblk[NL], varcol[NL];
   unsigned char stance[4 * MAXN];
-  unsigned char cflag[2 * NV + 8];  // active flag per constraint id (6 per stance foot-step)
+  unsigned char cflag[2 * NL + 8];  // active flag per constraint id (6 per stance foot-step)
 };
 
 __device__ __forceinline__ void lsync() {
@@ -117,11 +125,13 @@ __device__ __forceinline__ void pin(float (&x)[M]) {
     if (((c) & (CMPC_FENCE_COLS - 1)) == CMPC_FENCE_COLS - 4) __builtin_amdgcn_sched_barrier(0); \
   } while (0)
 
+template <int NV>
 __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KParams& P,
-                                         SharedC1& sh, float* __restrict__ fout,
+                                         SharedC1<NV>& sh, float* __restrict__ fout,
                                          uint8_t* __restrict__ st_out, int32_t* __restrict__ it_out,
                                          int* __restrict__ ovf_list, int* __restrict__ ovf_count,
                                          int inst) {
+  using G = C1Geo<NV>;
   const int v = threadIdx.x;
   const int N = P.N;
 #ifdef CMPC_PHASE_PROF
@@ -235,7 +245,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       gv = real ? 2.f * dot13(b, zk) : 0.f;  // qg = 2 B_qp' S (A_qp x0 + Q_qp f - X_d)
     }
     lsync();  // every ZE read is issued before P is overwritten
-    const int myrow = prow0(v);
+    const int myrow = G::prow0(v);
     float z[13];
 #pragma unroll
     for (int j = 0; j < 13; j++) z[j] = 0.f;
@@ -267,10 +277,11 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   // ---- row v of H into registers (full symmetric; identity padding for v >= n) ----------
   float slot[NV + 1];
   {
-    const int myrow = prow0(v);
+    const int vv = (v < NV) ? v : 0;  // lanes without a row read row 0 (and keep a zero row)
+    const int myrow = G::prow0(vv);
     static_for<0, NV>([&](auto C) {
       constexpr int c = decltype(C)::value;
-      const int addr = (c >= v) ? myrow + c : prow0(c) + v;
+      const int addr = (c >= vv) ? myrow + c : G::prow0(c) + vv;
       const float x = sh.P[addr];
       slot[c] = (real && c < n) ? x : ((c == v) ? 1.f : 0.f);
       if ((c & 7) == 7) __builtin_amdgcn_sched_barrier(0);
@@ -291,7 +302,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   float my_inv = 1.f;
   float dnext = 1.f, gnext = 0.f;
   if (n > 0) {
-    sh.P[prow(0) + v] = slot[0];
+    if (v < NV) sh.P[G::prow(0) + v] = slot[0];
     dnext = rl(slot[0], 0);
     gnext = rl(slot[NV], 0);
     lsync();
@@ -299,7 +310,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int c0 = k & ~3;
-    constexpr int rk = prow(k);
+    constexpr int rk = G::prow(k);
     constexpr int k1 = k + 1;
     constexpr int c1 = k1 & ~3;
     if (k < n) {
@@ -332,8 +343,8 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         }
         if constexpr (k1 < NV && c == c1) {
           if (k1 < n) {  // publish column k+1 (final after this chunk)
-            constexpr int rk1 = prow(k1);
-            if (v >= c1) sh.P[rk1 + v - c1] = (v >= k1) ? slot[k1] : 0.f;
+            constexpr int rk1 = G::prow(k1);
+            if (v >= c1 && v < NV) sh.P[rk1 + v - c1] = (v >= k1) ? slot[k1] : 0.f;
             dnext = rl(slot[k1], k1);
             gnext = rl(slot[NV], k1);
             lsync();
@@ -356,7 +367,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int c0 = k & ~3;
-    constexpr int rk = prow(k);
+    constexpr int rk = G::prow(k);
     if (k < n) {  // P and ibuf are read-only here: no per-step LDS ordering needed
       const float inv = sh.ibuf[k];
       const float xk = slot[k] * inv;
@@ -437,7 +448,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       // d = J' n+ : rows ia, iz of J through LDS (dword stores: wide stores would tie the row
       // registers into tuples)
       if (v == cp.ia || v == cp.iz) {  // both rows in one pass (two lanes per store)
-        const int boff = (v == cp.iz) ? NV : 0;  // bufB follows bufA
+        const int boff = (v == cp.iz) ? NL : 0;  // bufB follows bufA
 #pragma unroll
         for (int c = 0; c < NV; c++) {
           sh.bufA[boff + c] = slot[c];
@@ -607,26 +618,35 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 
 }  // namespace
 
+template <int NV>
 __global__ __launch_bounds__(64, CMPC_W1_WAVES_PER_EU) void cmpc_solve_c1_kernel(
     const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
-    uint8_t* __restrict__ status, int32_t* __restrict__ iters, int* __restrict__ ovf_list,
-    int* __restrict__ ovf_count) {
+    uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
+    const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
   // one instance per workgroup, no grid-stride loop: a loop around the solve would let LICM
   // hoist hundreds of lane-invariant addresses / masks out of it and spill them
-  __shared__ SharedC1 sh;
-  const int t = blockIdx.x;
-  if (t >= batch) return;
-  solve_c1(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * 12 * P.N, status + t,
-           iters ? iters + t : nullptr, ovf_list, ovf_count, t);
+  __shared__ SharedC1<NV> sh;
+  int t = blockIdx.x;
+  if (in_list) {  // list mode: workgroup i takes list entry i (surplus workgroups exit)
+    if (t >= *in_count) return;
+    t = in_list[t];
+  } else if (t >= batch) {
+    return;
+  }
+  solve_c1<NV>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * 12 * P.N, status + t,
+               iters ? iters + t : nullptr, ovf_list, ovf_count, t);
 }
 
-hipError_t launch_class1(const float* d_recs, int batch, const KParams& P, float* d_forces,
+hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream) {
-  (void)in_list;
-  (void)in_count;
-  hipLaunchKernelGGL(cmpc_solve_c1_kernel, dim3(grid), dim3(64), 0, stream, d_recs, batch, P,
-                     d_forces, d_status, d_iters, ovf_list, ovf_count);
+  if (grid <= 0) return hipSuccess;
+  if (nv == 60)
+    hipLaunchKernelGGL(cmpc_solve_c1_kernel<60>, dim3(grid), dim3(64), 0, stream, d_recs, batch, P,
+                       d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
+  else
+    hipLaunchKernelGGL(cmpc_solve_c1_kernel<64>, dim3(grid), dim3(64), 0, stream, d_recs, batch, P,
+                       d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
   return hipGetLastError();
 }
 

@@ -33,8 +33,12 @@ struct LocoParams {
 // Scratch ints needed by launch_solve for max_batch instances.
 // d_work: [0] instances with n > 64, [1..6] lengths of the class lists (wide classes of 80, 96,
 // 128, 192, 256 columns, general), [8 ..) the six lists of max_batch entries each
-constexpr int kLists = 7;  // 80, 96, 128, 192, 256, G, 144 (cnt[1 + list])
-inline size_t work_ints(int max_batch) { return 8 + kLists * (size_t)max_batch; }
+// instance lists of the classify pass: 80, 96, 128, 192, 256, G, 144, and 7: class-1 instances
+// with 60 < n <= 64 (the 64-wide class-1 build; n <= 60 runs in the 60-wide build over the
+// whole batch). d_work = [kHdr ints: cnt[0] total, cnt[1 + list]] [kLists lists of max_batch]
+constexpr int kLists = 8;
+constexpr int kHdr = 16;
+inline size_t work_ints(int max_batch) { return kHdr + kLists * (size_t)max_batch; }
 // Side streams and events of one handle: the wider size classes run concurrently with class 1
 // (they are latency-bound: few instances, long serial solves). Two side streams: with the
 // handle's own stream that is three of the four hardware queues a process gets by default
@@ -56,7 +60,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                         float* d_gscratch, hipStream_t stream, const LaunchCtx& ctx,
                         hipEvent_t* ev = nullptr);
 // per-class launchers (cmpc_class1.hip, cmpc_class2.hip, cmpc_classg.hip)
-hipError_t launch_class1(const float* d_recs, int batch, const KParams& P, float* d_forces,
+hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
 // 2-wavefront classes by row width (cmpc_class2_w{80,96,128}.hip)

@@ -20,7 +20,8 @@ namespace {
 // one thread per instance; wave-aggregated appends to the class lists
 __global__ __launch_bounds__(256) void cmpc_classify_kernel(const float* __restrict__ recs, int batch,
                                                             KParams P, int* __restrict__ cnt,
-                                                            int* __restrict__ lists, int max_batch) {
+                                                            int* __restrict__ lists, int max_batch,
+                                                            int c1_max) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   int cls = -1;
@@ -39,9 +40,9 @@ __global__ __launch_bounds__(256) void cmpc_classify_kernel(const float* __restr
     }
     const int n = 3 * nfs;
 #ifdef CMPC_LEGACY_C2
-    cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : 5;
+    cls = (n <= c1_max) ? -1 : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : 5;
 #else
-    cls = (n <= 64) ? -1 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : (n <= 144) ? 6
+    cls = (n <= c1_max) ? -1 : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : (n <= 144) ? 6
         : (n <= 192) ? 3 : (n <= 256) ? 4 : 5;
 #endif
   }
@@ -68,8 +69,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                         hipEvent_t* ev) {
   int* cnt = d_work;
   int* list[kLists];
-  for (int j = 0; j < kLists; j++) list[j] = d_work + 8 + (size_t)j * max_batch;
-  hipError_t e = hipMemsetAsync(d_work, 0, 8 * sizeof(int), stream);
+  for (int j = 0; j < kLists; j++) list[j] = d_work + kHdr + (size_t)j * max_batch;
+  hipError_t e = hipMemsetAsync(d_work, 0, kHdr * sizeof(int), stream);
   if (e != hipSuccess) return e;
   if (batch <= 0) {  // keep the timing slots consistent (zero-length launches)
     if (ev)
@@ -77,9 +78,15 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     return hipSuccess;
   }
   const int n_max = 12 * P.N;  // a class no instance of this horizon can reach is not launched
+  // Class 1 as two builds — 60-wide rows over the whole batch (n <= 60) and 64-wide rows over the
+  // classify list of 60 < n <= 64 — once the batch fills the GPU (config 3: 28.4 M -> 29.3 M
+  // QP/s). Below that the step is latency-bound and the extra kernel lengthens a side-stream
+  // chain (config 2, batch 4096: 11.2 M -> 9.9 M), so one 64-wide launch takes all n <= 64.
+  const bool split60 = (n_max <= 64) || (batch >= 16384);
+  const int c1_nv = (n_max <= 60 || split60) ? 60 : 64;
   if (n_max > 64) {
     hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_recs,
-                       batch, P, cnt, d_work + 8, max_batch);
+                       batch, P, cnt, d_work + kHdr, max_batch, c1_nv);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
     for (int s = 0; s < kSideStreams; s++)
@@ -96,13 +103,18 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     }();
     if (exact) {
       static int* h_cnt = nullptr;
-      if (!h_cnt && (e = hipHostMalloc(reinterpret_cast<void**>(&h_cnt), 8 * sizeof(int))) != hipSuccess)
+      if (!h_cnt && (e = hipHostMalloc(reinterpret_cast<void**>(&h_cnt), kHdr * sizeof(int))) != hipSuccess)
         return e;
-      if ((e = hipMemcpyAsync(h_cnt, cnt, 8 * sizeof(int), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      if ((e = hipMemcpyAsync(h_cnt, cnt, kHdr * sizeof(int), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
           (e = hipStreamSynchronize(stream)) != hipSuccess)
         return e;
       for (int j = 0; j < kLists; j++) grid_of[j] = h_cnt[1 + j];
     }
+    // the 64-wide class-1 build over its list (60 < n <= 64), ahead of the wide classes on side 1
+    // (side 0 carries the 80 class, the longest chain at N = 10)
+    if (split60 && (e = launch_class1(64, d_recs, batch, P, d_forces, d_status, d_iters, list[7],
+                                      &cnt[8], nullptr, nullptr, grid_of[7], ctx.side[1])) != hipSuccess)
+      return e;
 #ifdef CMPC_LEGACY_C2
     if ((e = launch_class2_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], nullptr,
                                nullptr, batch, ctx.side[0])) != hipSuccess)
@@ -144,7 +156,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       return e;
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
-  e = launch_class1(d_recs, batch, P, d_forces, d_status, d_iters, nullptr, nullptr, nullptr,
+  // class 1 over the whole batch (it skips instances with n > its row width)
+  e = launch_class1(c1_nv, d_recs, batch, P, d_forces, d_status, d_iters, nullptr, nullptr, nullptr,
                     nullptr, batch, stream);
   if (e != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
@@ -167,8 +180,8 @@ hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_f
   const int* cnt = d_one;
   const int* lst = d_one + 1;
   if (n <= 64)
-    return launch_class1(d_rec, 1, P, d_forces, d_status, d_iters, nullptr, nullptr, nullptr, nullptr,
-                         1, stream);
+    return launch_class1(n <= 60 ? 60 : 64, d_rec, 1, P, d_forces, d_status, d_iters, nullptr,
+                         nullptr, nullptr, nullptr, 1, stream);
   if (n <= 80) return launch_wide_w80(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
   if (n <= 96) return launch_wide_w96(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
   if (n <= 128) return launch_wide_w128(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
