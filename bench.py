@@ -277,7 +277,11 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
         t1 = float(np.mean(c1 + c2)) * 1e-3
         units1 = units_per_launch
     achieved = fl * units1 / t1 / 1e12 if t1 > 0 else None
-    traffic, pmc = load_pmc(N, units_per_launch, "cmpc_solve_c1_kernel" if not wide else "cmpc_solve_w_kernel<128>")
+    # class 1 runs as the 60-wide build once the batch fills the GPU (>= 16384 instances at
+    # N >= 6, cmpc_launch.hip), else as the 64-wide build
+    c1w = 60 if (units_per_launch >= 16384 or N <= 5) else 64
+    traffic, pmc = load_pmc(N, units_per_launch, f"cmpc_solve_c1_kernel<{c1w}>" if not wide
+                            else "cmpc_solve_w_kernel<128>")
     roofline = {
         "bound": "valu",
         "achieved": round(achieved, 3) if achieved else None,
@@ -285,7 +289,7 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
         "unit": "TFLOP/s",
         "frac": round(achieved / FP32_PEAK_TFLOPS, 5) if achieved else None,
         "traffic": traffic,
-        "kernel": ("cmpc_solve_c1_kernel<60> (n <= 60 class: 60-wide rows, one wavefront per instance)" if not wide
+        "kernel": (f"cmpc_solve_c1_kernel<{c1w}> (class 1, {c1w}-wide rows, one wavefront per instance)" if not wide
                    else "whole solve: every size class, concurrent streams"),
         "units_per_launch": int(units1),
         "flops_per_unit": fl,

@@ -1,7 +1,9 @@
 // cmpc_wide_w144.hip — wide size class with 144-column rows (n 129-144: random contact tables at N = 20) (kernel template: cmpc_wide.h).
 // two waves per SIMD: at three the 72-column half rows spill (25 VGPRs); five waves per
 // workgroup, 52 KB of LDS
+#ifndef CMPC_WIDE_WAVES_PER_EU
 #define CMPC_WIDE_WAVES_PER_EU 2
+#endif
 #include "cmpc_wide.h"
 
 namespace cmpc {
