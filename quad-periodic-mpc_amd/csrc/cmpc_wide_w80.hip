@@ -1,4 +1,9 @@
 // cmpc_wide_w80.hip — wide size class with 80-column rows (kernel template: cmpc_wide.h).
+// five waves per SIMD (96 VGPRs, one spilled): config 3's n 65-80 instances finish inside
+// class 1's run (tail beyond class 1 0.30 -> 0.15 ms, config 3 29.2M -> 29.6M QP/s)
+#ifndef CMPC_WIDE_WAVES_PER_EU
+#define CMPC_WIDE_WAVES_PER_EU 5
+#endif
 #include "cmpc_wide.h"
 
 namespace cmpc {
