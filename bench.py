@@ -44,8 +44,10 @@ sys.path.insert(0, ROOT)
 METRIC = "QP solves/sec (N=10, 13-state, 12-force) at batch=65536; 1/2/4/8 GPU"
 METRIC_C2 = "QP solves/sec (N=10) at batch=4096, 1 GPU (config 2)"
 METRIC_C5 = "QP solves/sec (N=20 + disturbance estimation, config 5) at batch=65536"
+METRIC_N16 = "QP solves/sec (N=16 trot, the deployed horizon) at batch=65536"
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (v_fma_f32 at 2 cyc/wave on SIMD-32)
 HBM_PEAK_GBS = 8000.0
+XGMI_LINK_GBS = 153.0      # one xGMI link, one direction (7 links per MI355X: SURVEY.md §5)
 
 
 def algorithmic_flops(N: int) -> float:
@@ -280,8 +282,9 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
     # class 1 runs as the 60-wide build once the batch fills the GPU (>= 16384 instances at
     # N >= 6, cmpc_launch.hip), else as the 64-wide build
     c1w = 60 if (units_per_launch >= 16384 or N <= 5) else 64
+    wide_k = f"cmpc_solve_w_kernel<{96 if N <= 16 else 128}>"   # the class that carries the batch
     traffic, pmc = load_pmc(N, units_per_launch, f"cmpc_solve_c1_kernel<{c1w}>" if not wide
-                            else "cmpc_solve_w_kernel<128>")
+                            else wide_k)
     roofline = {
         "bound": "valu",
         "achieved": round(achieved, 3) if achieved else None,
@@ -318,17 +321,77 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
     return roofline
 
 
+def scaling_model(args, cm, dev, sync):
+    """Config 4 at G = 1, 2, 4, 8 GPUs predicted from ONE GPU (a labelled model, not a
+    measurement): every rank of a G-GPU run solves 262144 / G records cut into
+    parallel.auto_chunks pieces, which a world-1 RootPipeline over that many records reproduces
+    exactly, so the per-rank solve time is measured here. Rank 0 scatters each piece's records to
+    G - 1 peers (one xGMI link each, concurrently) and gathers their forces back; only the first
+    scatter and the last gather are exposed, the rest overlaps the solve of the neighbouring
+    pieces unless it is longer than that solve. t_G = t_solve + t_first_scatter + t_last_gather
+    + max(0, comm of the inner pieces - t_solve); speedup = t_1 / t_G."""
+    import torch
+    par = importlib.import_module("quad-periodic-mpc_amd.parallel")
+    R = importlib.import_module("quad-periodic-mpc_amd.records")
+    N, G_total = 10, 262144
+    prm = cm.make_params(N)
+    rec_b = 4 * R.record_words(N)
+    out_b = 4 * 12 * N
+    recs_all = torch.from_numpy(cm.make_instances(G_total, N, random_contact_frac=args.random_contact_frac)).to(dev)
+    rows, t1 = [], None
+    for G in (1, 2, 4, 8):
+        local = G_total // G
+        pipe = par.RootPipeline(prm, local, device=dev)
+        recs = recs_all[:local]
+        for _ in range(3):
+            pipe.step(recs)
+        steps = 20
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            pipe.step(recs)
+        sync()
+        t_solve = (time.perf_counter() - t0) / steps
+        pieces = pipe.sizes
+        pipe.close()
+        row = {"gpus": G, "per_rank_instances": local, "pieces": len(pieces),
+               "piece_instances": pieces[0], "t_solve_ms_measured": round(t_solve * 1e3, 4)}
+        if G == 1:
+            t1 = t_solve
+            row.update(t_model_ms=round(t_solve * 1e3, 4), speedup=1.0)
+        else:
+            for bw, key in ((XGMI_LINK_GBS, ""), (50.0, "_at_50GBs")):
+                sc = [p * rec_b / (bw * 1e9) for p in pieces]   # per-peer bytes of a piece / link
+                ga = [p * out_b / (bw * 1e9) for p in pieces]
+                inner = sum(sc[1:]) + sum(ga[:-1])
+                t = t_solve + sc[0] + ga[-1] + max(0.0, inner - t_solve)
+                row["t_model_ms" + key] = round(t * 1e3, 4)
+                row["speedup" + key] = round(t1 / t, 3)
+            row["xgmi_mb_root_sends"] = round((G - 1) * local * rec_b / 1e6, 2)
+            row["xgmi_mb_root_receives"] = round((G - 1) * local * out_b / 1e6, 2)
+        rows.append(row)
+    del recs_all
+    return {"kind": "model (not a measurement): per-rank solve times measured on this GPU, "
+                    f"xGMI at {XGMI_LINK_GBS:.0f} GB/s per link and direction (and a pessimistic "
+                    "50 GB/s), comm overlap per parallel.RootPipeline",
+            "global_batch": G_total, "horizon": N, "rows": rows}
+
+
 def other_configs(args, cm, dev, rank, barrier, sync, dist):
-    """BASELINE configs 2 and 5 measured in the same (default, 1-GPU) run, after config 3, with
-    the same protocol: resident inputs, warmup, barrier + synchronize, HIP-event roofline."""
+    """BASELINE configs 2 and 5, and the deployed horizon N = 16 (ros_config.yaml:93, trot), measured
+    in the same (default, 1-GPU) run after config 3, with the same protocol: resident inputs,
+    warmup, barrier + synchronize, HIP-event roofline."""
     out = {}
-    for config, N, B, steps, warmup in ((2, 10, 4096, 200, 20), (5, 20, 65536, 5, 2)):
+    legs = ((2, 10, 4096, 200, 20, None), ("n16_trot", 16, 65536, 20, 3, 0.0), (5, 20, 65536, 5, 2, None))
+    for config, N, B, steps, warmup, frac in legs:
         prm = cm.make_params(N)
-        leg = local_leg(args, cm, prm, config, N, B, steps, warmup, dev, rank, barrier, sync, dist)
+        leg = local_leg(args, cm, prm, config, N, B, steps, warmup, dev, rank, barrier, sync, dist,
+                        frac=frac)
         launch_ms, ovf = leg["solver"].read_timing()
         value = B * steps / leg["elapsed"]
         st = np.bincount(leg["status"].cpu().numpy(), minlength=5)
-        d = {"metric": METRIC_C2 if config == 2 else METRIC_C5, "value": round(value, 1),
+        metric = {2: METRIC_C2, 5: METRIC_C5}.get(config, METRIC_N16)
+        d = {"metric": metric, "value": round(value, 1),
              "unit": "QP solves/s", "ms_per_step": round(leg["elapsed"] / steps * 1e3, 4),
              "steps": steps, "warmup": warmup, "batch": B, "horizon": N,
              "roofline": make_roofline(launch_ms, ovf, B, N, value, config),
@@ -340,11 +403,15 @@ def other_configs(args, cm, dev, rank, barrier, sync, dist):
                              "the solve, histories at 400..405 samples")
             if not args.no_cpu_baseline:
                 d["cpu_baseline"] = cpu_baseline(prm, N, config5=True)
-        else:
+        elif config == 2:
             d["workload"] = "N=10, batch 4096 (same instance mix as config 3)"
             d["cpu_baseline"] = "same per-instance workload as config 3: see cpu_baseline"
+        else:
+            d["workload"] = ("N=16, batch 65536, A1 trot at random phase (every instance n = 96 "
+                             "reduced variables): the reference's deployed operating point "
+                             "(ros_config.yaml:93), not a BASELINE config")
         leg["solver"].close()
-        out[f"config{config}"] = d
+        out[f"config{config}" if isinstance(config, int) else config] = d
     return out
 
 
@@ -357,7 +424,8 @@ def main():
     ap.add_argument("--config5", action="store_true", help="alias of --config 5")
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (configs 2, 3, 5)")
     ap.add_argument("--global-batch", type=int, default=None, help="total instances (config 4)")
-    ap.add_argument("--chunks", type=int, default=4, help="config-4 pipeline pieces per rank")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="config-4 pipeline pieces per rank (default: parallel.auto_chunks)")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--random-contact-frac", type=float, default=0.25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -498,6 +566,7 @@ def main():
             solver.close()
             solver = None
         extras["other_configs"] = other_configs(args, cm, dev, rank, barrier, sync, dist)
+        extras["scaling_model"] = scaling_model(args, cm, dev, sync)
     status_counts = None
     if st_local is not None:
         sc = np.bincount(st_local.cpu().numpy(), minlength=5)

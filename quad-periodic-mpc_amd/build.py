@@ -18,8 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcmpc_hip.so")
 OBJ = os.path.join(ROOT, "build", "obj")
 # one translation unit per kernel family so the large unrolled kernels compile in parallel
-SOURCES = ["cmpc_class1.hip", "cmpc_class2_w80.hip", "cmpc_class2_w96.hip", "cmpc_class2_w128.hip",
-           "cmpc_wide_w80.hip", "cmpc_wide_w96.hip", "cmpc_wide_w128.hip", "cmpc_wide_w144.hip", "cmpc_wide_w192.hip",
+SOURCES = ["cmpc_class1.hip", "cmpc_wide_w80.hip", "cmpc_wide_w96.hip", "cmpc_wide_w128.hip", "cmpc_wide_w144.hip", "cmpc_wide_w192.hip",
            "cmpc_wide_w256.hip", "cmpc_classg.hip", "cmpc_launch.hip", "cmpc_estimator.hip", "cmpc_assemble.hip",
            "cmpc_admm.hip", "cmpc_quadprog.hip", "cmpc_abi.cpp"]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")

@@ -41,6 +41,8 @@ struct cmpc_batch {
   double* d_admm_slabs = nullptr;  // ADMM inverses of QPs with n > 120 (cmpc_admm.hip)
   size_t admm_slab_doubles = 0;
   int admm_nslabs = 0;
+  bool admm_used = false;        // slabs are allocated on the first ADMM call, not at create
+  bool staged = false;           // every allocation of ensure_staging succeeded
   float* d_admm_H = nullptr;     // condensed qH / qg staging of the single-instance ADMM path
   // staging for the host-pointer entry point (allocated lazily, sized max_batch)
   float* d_rec = nullptr;
@@ -106,9 +108,12 @@ static int ensure_gscratch(cmpc_batch* h) {
 }
 
 // the ADMM kernel keeps M^-1 of QPs with more than 120 variables in per-workgroup fp64 slabs:
-// min(max_batch, kAdmmSlabs) of (12N)^2 doubles, allocated here, never inside a solve
+// min(max_batch, kAdmmSlabs) of (12N)^2 doubles (151 MB at N = 16, 236 MB at N = 20). They are
+// allocated by the first cmpc_batch_admm call of a handle (and kept across set_params from then
+// on), so handles that only run the default qpOASES-equivalent solve never pay for them; the
+// solve kernels themselves never allocate.
 static int ensure_admm_slabs(cmpc_batch* h) {
-  if (h->max_batch <= 0 || 12 * h->prm.horizon <= 120) return 0;
+  if (!h->admm_used || h->max_batch <= 0 || 12 * h->prm.horizon <= 120) return 0;
   const int ns = h->max_batch < cmpc::kAdmmSlabs ? h->max_batch : cmpc::kAdmmSlabs;
   const size_t need = (size_t)ns * cmpc::admm_slab_doubles(h->prm.horizon);
   if (need <= h->admm_slab_doubles && h->admm_nslabs >= ns) return 0;
@@ -175,10 +180,11 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
     if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("gauss taps", e); }
   }
   if (int r = ensure_gscratch(h); r != 0) { cmpc_batch_destroy(h); return r; }
-  if (int r = ensure_admm_slabs(h); r != 0) { cmpc_batch_destroy(h); return r; }
   *out = h;
   return 0;
 }
+
+static void free_staging(cmpc_batch* h);
 
 extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (!h) return;
@@ -186,14 +192,7 @@ extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (h->d_gscratch) (void)hipFree(h->d_gscratch);
   if (h->d_gauss) (void)hipFree(h->d_gauss);
   if (h->d_admm_slabs) (void)hipFree(h->d_admm_slabs);
-  if (h->d_admm_H) (void)hipFree(h->d_admm_H);
-  if (h->d_rec) (void)hipFree(h->d_rec);
-  if (h->d_forces) (void)hipFree(h->d_forces);
-  if (h->d_status) (void)hipFree(h->d_status);
-  if (h->d_iters) (void)hipFree(h->d_iters);
-  if (h->d_one) (void)hipFree(h->d_one);
-  if (h->d_single_out) (void)hipFree(h->d_single_out);
-  if (h->h_pin) (void)hipHostFree(h->h_pin);
+  free_staging(h);
   for (auto e : h->ev) (void)hipEventDestroy(e);
   for (int j = 0; j < cmpc::kSideStreams; j++) {
     if (h->ctx.side[j]) (void)hipStreamDestroy(h->ctx.side[j]);
@@ -317,33 +316,57 @@ extern "C" int cmpc_batch_admm(cmpc_batch* h, const float* d_records, const floa
     g_last_error = "cmpc_batch_admm: bad arguments";
     return -1;
   }
+  if (!h->admm_used) {
+    h->admm_used = true;
+    if (int r = ensure_admm_slabs(h)) { h->admm_used = false; return r; }
+  }
   hipError_t e = cmpc::launch_admm(d_records, d_H, d_g, batch, h->kp, *s, d_forces, d_status,
                                    d_iters, h->d_admm_slabs, h->admm_nslabs, h->stream);
   if (e != hipSuccess) return fail("launch_admm", e);
   return 0;
 }
 
+static void free_staging(cmpc_batch* h) {
+  if (h->d_rec) (void)hipFree(h->d_rec);
+  if (h->d_forces) (void)hipFree(h->d_forces);
+  if (h->d_status) (void)hipFree(h->d_status);
+  if (h->d_iters) (void)hipFree(h->d_iters);
+  if (h->d_admm_H) (void)hipFree(h->d_admm_H);
+  if (h->d_one) (void)hipFree(h->d_one);
+  if (h->d_single_out) (void)hipFree(h->d_single_out);
+  if (h->h_pin) (void)hipHostFree(h->h_pin);
+  h->d_rec = h->d_forces = h->d_admm_H = h->d_single_out = h->h_pin = nullptr;
+  h->d_status = nullptr;
+  h->d_iters = nullptr;
+  h->d_one = nullptr;
+  h->staged = false;
+}
+
+// staging of the host-pointer entry points, allocated on first use; all or nothing (a failed
+// allocation frees what was allocated, so a later call retries instead of using null buffers)
 static int ensure_staging(cmpc_batch* h) {
-  if (h->d_rec) return 0;
+  if (h->staged) return 0;
   const size_t words = (size_t)CMPC_REC_WORDS(CMPC_MAX_HORIZON) * h->max_batch;
-  hipError_t e;
-  if ((e = hipMalloc(&h->d_rec, words * sizeof(float))) != hipSuccess) return fail("hipMalloc", e);
-  if ((e = hipMalloc(&h->d_forces, (size_t)12 * CMPC_MAX_HORIZON * h->max_batch * sizeof(float))) != hipSuccess)
-    return fail("hipMalloc", e);
-  if ((e = hipMalloc(&h->d_status, (size_t)h->max_batch)) != hipSuccess) return fail("hipMalloc", e);
-  if ((e = hipMalloc(&h->d_iters, sizeof(int32_t) * h->max_batch)) != hipSuccess) return fail("hipMalloc", e);
-  // qH / qg of one instance at the largest horizon (the single-instance ADMM path)
-  const size_t nv = 12 * (size_t)CMPC_MAX_HORIZON;
-  if ((e = hipMalloc(&h->d_admm_H, (nv * nv + nv) * sizeof(float))) != hipSuccess) return fail("hipMalloc", e);
+  const size_t nv = 12 * (size_t)CMPC_MAX_HORIZON;  // qH / qg of one instance (single ADMM path)
   const int one[2] = {1, 0};
-  if ((e = hipMalloc(&h->d_one, sizeof(one))) != hipSuccess) return fail("hipMalloc", e);
-  if ((e = hipMemcpy(h->d_one, one, sizeof(one), hipMemcpyHostToDevice)) != hipSuccess) return fail("H2D", e);
-  if ((e = hipMalloc(&h->d_single_out, (12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) != hipSuccess)
-    return fail("hipMalloc", e);
-  if ((e = hipHostMalloc(reinterpret_cast<void**>(&h->h_pin),
-                         (CMPC_REC_WORDS(CMPC_MAX_HORIZON) + 12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) != hipSuccess)
-    return fail("hipHostMalloc", e);
-  return 0;
+  hipError_t e;
+  const char* what = "hipMalloc";
+  if ((e = hipMalloc(&h->d_rec, words * sizeof(float))) == hipSuccess &&
+      (e = hipMalloc(&h->d_forces, (size_t)12 * CMPC_MAX_HORIZON * h->max_batch * sizeof(float))) == hipSuccess &&
+      (e = hipMalloc(&h->d_status, (size_t)h->max_batch)) == hipSuccess &&
+      (e = hipMalloc(&h->d_iters, sizeof(int32_t) * h->max_batch)) == hipSuccess &&
+      (e = hipMalloc(&h->d_admm_H, (nv * nv + nv) * sizeof(float))) == hipSuccess &&
+      (e = hipMalloc(&h->d_one, sizeof(one))) == hipSuccess &&
+      (e = hipMalloc(&h->d_single_out, (12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) == hipSuccess &&
+      (what = "hipHostMalloc",
+       e = hipHostMalloc(reinterpret_cast<void**>(&h->h_pin),
+                         (CMPC_REC_WORDS(CMPC_MAX_HORIZON) + 12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) == hipSuccess &&
+      (what = "H2D", e = hipMemcpy(h->d_one, one, sizeof(one), hipMemcpyHostToDevice)) == hipSuccess) {
+    h->staged = true;
+    return 0;
+  }
+  free_staging(h);
+  return fail(what, e);
 }
 
 // reduced size n = 3 x (stance foot-steps) of one record: eliminated iff |gait * f_max| < 0.01,

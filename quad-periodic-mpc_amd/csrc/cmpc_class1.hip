@@ -25,7 +25,7 @@
 #include "cmpc_common.h"
 
 #ifndef CMPC_W1_WAVES_PER_EU
-#define CMPC_W1_WAVES_PER_EU 2
+#define CMPC_W1_WAVES_PER_EU 4
 #endif
 // Cholesky sweep chunks (of every 4) whose column broadcast goes through v_readlane instead of
 // the LDS (see the Cholesky stage)
@@ -76,23 +76,33 @@ constexpr int OFF_E = 0;
 constexpr int OFF_ZE = OFF_E + 16 * MAXN;
 constexpr int OFF_REC = OFF_ZE + 16 * MAXN;  // LDS copy of the instance record (16-B aligned)
 
+// stance foot-steps a class-1 instance can have (n = 3 x stance <= 64); the stance scan stores
+// only that many (an instance with more is handed on before they are read)
+constexpr int C1_MAXFS = 24;
+
 template <int NV>
 struct SharedC1 {
   static_assert(NV % 4 == 0 && NV <= NL, "row width");
   static_assert(NV * (NV + 1) / 2 <= C1Geo<NV>::PSZ, "R must fit in P");
   static_assert(OFF_REC + CMPC_REC_WORDS(MAXN) <= C1Geo<NV>::PSZ, "prep scratch must fit in P");
+  static_assert(3 * C1_MAXFS >= NV, "stance list");
   float P[C1Geo<NV>::PSZ];
-  float BdtT[12][16];
-  float ibuf[NL];          // 1 / sqrt(d_k) of pivot k
+  // arrays of different stages share one region: 10 KB of LDS per instance at NV = 60, so
+  // sixteen one-wave workgroups (four waves per SIMD) fit a CU's 160 KB
+  union {
+    float BdtT[12][16];    // prep + condensation: Bdt transposed
+    float ibuf[NL];        // Cholesky + J: 1 / sqrt(d_k) of pivot k
+    struct {               // active set
+      float bufA[NL], bufB[NL];  // published J rows ia, iz (contiguous: bufA[NL + c] = bufB[c])
+      float xs[NL];
+      float cs[2 * NL];    // Givens (c, s) per column pair
+    } gi;
+  } u;
   float vbuf[NL];          // broadcast vector (y, then masked d)
-  float bufA[NL], bufB[NL];  // published J rows ia, iz (contiguous: bufA[NL + c] = bufB[c])
-  float xs[NL];
-  float cs[2 * NL];        // Givens (c, s) per column pair
-  float sub[4 * MAXN];     // ub of each stance foot-step (gait * f_max)
-  int sfs[4 * MAXN];       // stance foot-step ids, in order
+  float sub[C1_MAXFS];     // ub of each stance foot-step (gait * f_max)
+  int sfs[C1_MAXFS];       // stance foot-step ids, in order
   int blkbase[MAXN + 2];   // first reduced variable of each horizon step
   unsigned char varblk[NL], varcol[NL];
-  unsigned char stance[4 * MAXN];
   unsigned char cflag[2 * NL + 8];  // active flag per constraint id (6 per stance foot-step)
 };
 
@@ -158,12 +168,11 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     if (t < 4 * N) {
       ub = (float)gait[t] * P.f_max;
       f = !(ub < 0.01f && ub > -0.01f);
-      sh.stance[t] = f ? 1 : 0;
     }
     const unsigned long long m = __ballot(f);
     if (c0 == 0) msk0 = m; else msk1 = m;
     const int pre = __popcll(m & ((1ull << v) - 1ull));
-    if (f) {
+    if (f && nfs + pre < C1_MAXFS) {
       sh.sfs[nfs + pre] = t;
       sh.sub[nfs + pre] = ub;
     }
@@ -194,7 +203,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   }
   Model md;
   make_model(srec, P.dt, md);
-  make_bdt<64>(srec, md, v, sh.BdtT);
+  make_bdt<64>(srec, md, v, sh.u.BdtT);
   lsync();
   if (v < N) {
     float e[13];
@@ -235,7 +244,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     const int cv = real ? sh.varcol[v] : 0;
     float b[13], u1[13], u2[13];
 #pragma unroll
-    for (int j = 0; j < 13; j++) b[j] = real ? sh.BdtT[cv][j] : 0.f;
+    for (int j = 0; j < 13; j++) b[j] = real ? sh.u.BdtT[cv][j] : 0.f;
     n1_mul(md, b, u1);
     n1_mul(md, u1, u2);
     {
@@ -264,7 +273,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         const int cw = sh.varcol[w];
         float bw[13];
 #pragma unroll
-        for (int j = 0; j < 13; j++) bw[j] = sh.BdtT[cw][j];
+        for (int j = 0; j < 13; j++) bw[j] = sh.u.BdtT[cw][j];
         float val = 2.f * dot13(bw, z);
         if (w == v) val += P.alpha2;  // qH = 2 (B'SB + alpha I), SolverMPC.cpp:806
         if (act && w >= v) sh.P[myrow + w] = val;
@@ -318,7 +327,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       const float gk = gnext;
       if (!(d > 0.f)) { status = CMPC_NOT_PD; d = 1e-30f; }
       const float inv = __builtin_amdgcn_rsqf(d);  // d is a normal positive pivot
-      if (v == k) { my_inv = inv; sh.ibuf[k] = inv; }
+      if (v == k) { my_inv = inv; sh.u.ibuf[k] = inv; }
       const float colk = slot[k];  // lane c holds the raw column entry of row c
       const float a = (v > k) ? -colk * (inv * inv) : 0.f;
       slot[NV] = fmaf(a, gk, slot[NV]);
@@ -369,7 +378,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     constexpr int c0 = k & ~3;
     constexpr int rk = G::prow(k);
     if (k < n) {  // P and ibuf are read-only here: no per-step LDS ordering needed
-      const float inv = sh.ibuf[k];
+      const float inv = sh.u.ibuf[k];
       const float xk = slot[k] * inv;
       const float a = -xk * inv;
 #pragma unroll
@@ -419,12 +428,12 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       pin(slot);
       const int v = tid_opq();  // re-materialised: keeps per-lane addresses out of the preheader
       if (p < 0) {
-        sh.xs[v] = xv;
+        sh.u.gi.xs[v] = xv;
         lsync();
         float best = 0.f;
         int bid = 0x7fffffff;
         if (v < nfs) {
-          const float fx = sh.xs[3 * v], fy = sh.xs[3 * v + 1], fz = sh.xs[3 * v + 2];
+          const float fx = sh.u.gi.xs[3 * v], fy = sh.u.gi.xs[3 * v + 1], fz = sh.u.gi.xs[3 * v + 2];
           float sl[6];
           sl[0] = (mui * fx + fz) * fnorm;
           sl[1] = (-mui * fx + fz) * fnorm;
@@ -451,12 +460,12 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         const int boff = (v == cp.iz) ? NL : 0;  // bufB follows bufA
 #pragma unroll
         for (int c = 0; c < NV; c++) {
-          sh.bufA[boff + c] = slot[c];
+          sh.u.gi.bufA[boff + c] = slot[c];
           if ((c & 15) == 15) __builtin_amdgcn_sched_barrier(0);
         }
       }
       lsync();
-      const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[v], cp.cb * sh.bufB[v]) : cp.cb * sh.bufB[v];
+      const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.u.gi.bufA[v], cp.cb * sh.u.gi.bufB[v]) : cp.cb * sh.u.gi.bufB[v];
       const float dm = (v >= q && v < n) ? dv : 0.f;
       sh.vbuf[v] = dm;
       lsync();
@@ -469,7 +478,10 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
         CMPC_SWEEP_FENCE(c);
       }
-      const float zv = zacc.x + zacc.y, zn = nacc.x + nacc.y;
+      float zv = zacc.x + zacc.y, zn = nacc.x + nacc.y;
+      // materialise both sums here: otherwise the FMAs sink below the back substitution loop
+      // and the NV loaded values of vbuf stay live across it (158 VGPRs, three waves per SIMD)
+      asm volatile("" : "+v"(zv), "+v"(zn));
       const float dn = wave_sum((v < n) ? dv * dv : 0.f);
       // r = R^-1 d1: back substitution over the packed columns of R (lane i ends with r_i)
       float acc = dv, r_reg = 0.f;
@@ -502,7 +514,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         const float sgn = (dq >= 0.f) ? 1.f : -1.f;
         beta = fast_rcp(ts * (ts + fabsf(dq)));  // 2 / (w'w)
         sh.vbuf[v] = (v == q) ? dq + sgn * ts : dm;
-        *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(1.f, 0.f);
+        *reinterpret_cast<float2*>(&sh.u.gi.cs[2 * v]) = make_float2(1.f, 0.f);
         const int offq = rcol(q);
         if (v < q) sh.P[offq + v] = dv;
         if (v == q) {
@@ -522,7 +534,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         const int a_nx = lane_next_i(act_reg, act_reg);
         const float u_nx = lane_next(u_reg, u_reg);
         if (v >= k && v < q - 1) { act_reg = a_nx; u_reg = u_nx; }
-        if (v < k || v > q - 2) *reinterpret_cast<float2*>(&sh.cs[2 * v]) = make_float2(1.f, 0.f);
+        if (v < k || v > q - 2) *reinterpret_cast<float2*>(&sh.u.gi.cs[2 * v]) = make_float2(1.f, 0.f);
         const bool in_c = v >= k && v <= q - 2;
         float top = in_c ? sh.P[rcol(v + 1) + k] : 0.f;
         lsync();
@@ -544,7 +556,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
             sh.P[rcol(v) + j] = fmaf(cc, top, sn * bot);
             top = fmaf(-sn, top, cc * bot);
           }
-          if (v == 0) *reinterpret_cast<float2*>(&sh.cs[2 * j]) = make_float2(cc, sn);
+          if (v == 0) *reinterpret_cast<float2*>(&sh.u.gi.cs[2 * j]) = make_float2(cc, sn);
           lsync();
         }
       }
@@ -575,7 +587,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         // J columns (j, j+1) <- Givens chain j = 0 .. NV-2 (identity on an add)
         static_for<0, NV - 1>([&](auto JC) {
           constexpr int j = decltype(JC)::value;
-          const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs[2 * j]);
+          const float2 cs2 = *reinterpret_cast<const float2*>(&sh.u.gi.cs[2 * j]);
           const float x0 = slot[j], x1 = slot[j + 1];
           slot[j] = fmaf(cs2.x, x0, cs2.y * x1);
           slot[j + 1] = fmaf(-cs2.y, x0, cs2.x * x1);

@@ -135,37 +135,21 @@ __device__ __forceinline__ int opaque(int x) {
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // Row-sweep helpers: x[0..3] += a * r[0..3] and acc += x[0..3] . r[0..3] (acc is a lane pair,
-// summed once at the end). Scalar FMAs by default; -DCMPC_PK builds them from packed FP32
-// (v_pk_fma_f32), which was measured 20 % slower in class 1 (2.47 vs 2.03 ms: packing the row
-// registers into pairs costs more moves than the halved FMA count saves).
+// summed once at the end). Scalar FMAs: packed FP32 (v_pk_fma_f32) was measured 20 % slower in
+// class 1 (2.47 vs 2.03 ms: packing the row registers into pairs costs more moves than the
+// halved FMA count saves).
 typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void axpy4(float a, float4 r, float& x0, float& x1, float& x2, float& x3) {
-#ifndef CMPC_PK
   x0 = fmaf(a, r.x, x0);
   x1 = fmaf(a, r.y, x1);
   x2 = fmaf(a, r.z, x2);
   x3 = fmaf(a, r.w, x3);
-#else
-  const f2v aa = {a, a};
-  f2v lo = {x0, x1}, hi = {x2, x3};
-  lo = __builtin_elementwise_fma(aa, f2v{r.x, r.y}, lo);
-  hi = __builtin_elementwise_fma(aa, f2v{r.z, r.w}, hi);
-  x0 = lo.x;
-  x1 = lo.y;
-  x2 = hi.x;
-  x3 = hi.y;
-#endif
 }
 __device__ __forceinline__ void dot4(f2v& acc, float x0, float x1, float x2, float x3, float4 r) {
-#ifndef CMPC_PK
   acc.x = fmaf(x0, r.x, acc.x);
   acc.x = fmaf(x1, r.y, acc.x);
   acc.x = fmaf(x2, r.z, acc.x);
   acc.x = fmaf(x3, r.w, acc.x);
-#else
-  acc = __builtin_elementwise_fma(f2v{x0, x1}, f2v{r.x, r.y}, acc);
-  acc = __builtin_elementwise_fma(f2v{x2, x3}, f2v{r.z, r.w}, acc);
-#endif
 }
 
 // single-wavefront workgroup: orders this wave's LDS traffic without an s_barrier

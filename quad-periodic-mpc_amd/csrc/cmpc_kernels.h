@@ -59,20 +59,10 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
                         float* d_gscratch, hipStream_t stream, const LaunchCtx& ctx,
                         hipEvent_t* ev = nullptr);
-// per-class launchers (cmpc_class1.hip, cmpc_class2.hip, cmpc_classg.hip)
+// per-class launchers (cmpc_class1.hip, cmpc_wide_w*.hip, cmpc_classg.hip)
 hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
-// 2-wavefront classes by row width (cmpc_class2_w{80,96,128}.hip)
-#define CMPC_DECL_CLASS2(W)                                                                        \
-  hipError_t launch_class2_w##W(const float* d_recs, const KParams& P, float* d_forces,           \
-                                uint8_t* d_status, int32_t* d_iters, const int* in_list,          \
-                                const int* in_count, int* ovf_list, int* ovf_count, int grid,     \
-                                hipStream_t stream);
-CMPC_DECL_CLASS2(80)
-CMPC_DECL_CLASS2(96)
-CMPC_DECL_CLASS2(128)
-#undef CMPC_DECL_CLASS2
 // wide classes, two lanes per row, NV/32 wavefronts (cmpc_wide_w{80,96,128,144,192,256}.hip)
 #define CMPC_DECL_WIDE(W)                                                                          \
   hipError_t launch_wide_w##W(const float* d_recs, const KParams& P, float* d_forces,             \

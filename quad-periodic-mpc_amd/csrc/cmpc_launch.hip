@@ -7,8 +7,6 @@
 //     streams forked after classify, so they run concurrently with class 1 and with each
 //     other. At N = 10 they are a latency-bound tail (few, long solves); at N = 16..20 the 128-
 //     and 192-column classes carry the batch and run side by side on the two streams.
-//   -DCMPC_LEGACY_C2 builds the round-1 arrangement instead (one lane per row, 2-wavefront
-//     classes of 80 / 96 / 128 columns, G above 128) for A/B measurements.
 #include <stdlib.h>
 
 #include "cmpc_kernels.h"
@@ -39,12 +37,8 @@ __global__ __launch_bounds__(256) void cmpc_classify_kernel(const float* __restr
       }
     }
     const int n = 3 * nfs;
-#ifdef CMPC_LEGACY_C2
-    cls = (n <= c1_max) ? -1 : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : 5;
-#else
     cls = (n <= c1_max) ? -1 : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : (n <= 144) ? 6
         : (n <= 192) ? 3 : (n <= 256) ? 4 : 5;
-#endif
   }
   const unsigned long long any = __ballot(cls >= 0);
   if (any == 0ull) return;
@@ -115,18 +109,6 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if (split60 && (e = launch_class1(64, d_recs, batch, P, d_forces, d_status, d_iters, list[7],
                                       &cnt[8], nullptr, nullptr, grid_of[7], ctx.side[1])) != hipSuccess)
       return e;
-#ifdef CMPC_LEGACY_C2
-    if ((e = launch_class2_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], nullptr,
-                               nullptr, batch, ctx.side[0])) != hipSuccess)
-      return e;
-    if (n_max > 80 && (e = launch_class2_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2],
-                                             nullptr, nullptr, batch, ctx.side[1])) != hipSuccess)
-      return e;
-    if (n_max > 96 && (e = launch_class2_w128(d_recs, P, d_forces, d_status, d_iters, list[2],
-                                              &cnt[3], nullptr, nullptr, batch, ctx.side[1])) != hipSuccess)
-      return e;
-    const bool g_possible = n_max > 128;
-#else
     // side 0: 80, 128, 256; side 1: 96, 144, 192 (at N = 20 the 128-column class and the
     // 144/192-column classes, which carry the batch, run side by side)
     if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], grid_of[0],
@@ -149,7 +131,6 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                                              grid_of[4], ctx.side[0])) != hipSuccess)
       return e;
     const bool g_possible = n_max > 256;
-#endif
     if (g_possible && (e = launch_classg(d_recs, batch, P, d_forces, d_status, d_iters, list[5],
                                          &cnt[6], d_gscratch, classg_grid(max_batch),
                                          ctx.side[1])) != hipSuccess)

@@ -140,6 +140,13 @@ __device__ __forceinline__ void wpin(float (&x)[M]) {
   do {                                                       \
     if (((c) & 15) == 12) __builtin_amdgcn_sched_barrier(0); \
   } while (0)
+// the active-set loop's sweeps over LDS vectors: 8 columns between fences for half rows of <= 48
+// columns (the 16 loaded values of a 16-column chunk were the loop's register peak: w96 fits
+// 96 VGPRs, five waves per SIMD, without spills), 16 otherwise (kGiFence in solve_w)
+#define CMPC_WGI_FENCE(c)                                                      \
+  do {                                                                         \
+    if (((c) & (kGiFence - 1)) == kGiFence - 4) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
 
 // readlane of position i (0 <= i < 64 RQ) of a per-lane array of RQ registers (i uniform)
 template <int RQ>
@@ -168,6 +175,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   using G = WGeo<NV>;
   constexpr int NH = G::NH;
   constexpr int RQ = G::RQ;
+  constexpr int kGiFence = (NH <= 48) ? 8 : 16;
   const int t = tid_opq();  // opaque: nothing lane-dependent is hoisted out of the persistent loop
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -366,10 +374,17 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
 #if CMPC_DIAG_STOP != 1  // diagnostic builds: stop after the Cholesky (1) / after J (2)
   // ---- J = L^-T: row r solves L x = e_r over its half of the columns (LDS reads only; the
   // pivot value x_k lives in the half holding column k: one partner exchange per step)
-  static_for<0, NH>([&](auto J) {
-    constexpr int j = decltype(J)::value;
-    slot[j] = (2 * j + h == r) ? 1.f : 0.f;
-  });
+  {
+    // the unit row from an opaque thread index: with the plain (h, r) the NH per-lane column
+    // ids 2 j + h are shared (CSE) with the H-row load above and stay live across the whole
+    // Cholesky (64 VGPRs at NV = 128)
+    const int to = tid_opq();
+    const int lr = ((to & 63) >> 5) - 32 * (to >> 6) - (to & 31);  // h - r
+    static_for<0, NH>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      slot[j] = (lr == -2 * j) ? 1.f : 0.f;
+    });
+  }
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int kj = k >> 1, kh = k & 1;
@@ -501,10 +516,13 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
           const float4 m4 = *reinterpret_cast<const float4*>(vb + j);
           dot4(zacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], m4);
           dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
-          CMPC_WSWEEP_FENCE(j);
+          CMPC_WGI_FENCE(j);
         }
         zv = pair_sum(zacc.x + zacc.y);
         zn = pair_sum(nacc.x + nacc.y);
+        // materialise both sums here: otherwise the FMAs sink below wave 0's back substitution
+        // and the NV/2 loaded values of vbuf stay live across it
+        asm volatile("" : "+v"(zv), "+v"(zn));
 #pragma unroll
         for (int w = 0; w < G::NW; w++) dn += sh.redf[w];
       }
@@ -667,7 +685,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         for (int j = 0; j < NH; j += 4) {
           const float4 w4 = *reinterpret_cast<const float4*>(vb + j);
           dot4(tacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], w4);
-          CMPC_WSWEEP_FENCE(j);
+          CMPC_WGI_FENCE(j);
         }
         const float bt = -beta * pair_sum(tacc.x + tacc.y);
         asm volatile("" ::: "memory");
@@ -675,7 +693,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         for (int j = 0; j < NH; j += 4) {
           const float4 w4 = *reinterpret_cast<const float4*>(vb + j);
           axpy4(bt, w4, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
-          CMPC_WSWEEP_FENCE(j);
+          CMPC_WGI_FENCE(j);
         }
       }
       // J columns (l, l+1) <- Givens chain, ascending l (identity on an add)
@@ -745,27 +763,21 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
 }  // namespace
 
 // One workgroup per possible entry of the class's list (the list length is only known on the
-// device); surplus workgroups exit after one load. -DCMPC_WIDE_PERSIST=1 builds persistent
-// workgroups instead, which dequeue entries by decrementing the list length (grid sized to the
-// machine, wide_grid): measured to spill (w128: 168 VGPRs + 48 spilled, 256 SGPR spills, against
-// 159 VGPRs and no spills for one solve per workgroup), so it is off.
-#ifndef CMPC_WIDE_PERSIST
-#define CMPC_WIDE_PERSIST 0
-#endif
+// device); surplus workgroups exit after one load. (Persistent workgroups that dequeue list
+// entries were measured to spill — w128: 168 VGPRs + 48 spilled, 256 SGPR spills — and were
+// dropped.)
 #if CMPC_WIDE_VGPR_CAP > 0
 #define CMPC_WIDE_VGPR_ATTR __attribute__((amdgpu_num_vgpr(CMPC_WIDE_VGPR_CAP)))
 #else
 #define CMPC_WIDE_VGPR_ATTR
 #endif
-// Kernel arguments as one struct, so the persistent loop can re-read all of them per instance
-// through a single opaque kernarg pointer (below)
 struct WideArgs {
   const float* recs;
   float* forces;
   uint8_t* status;
   int32_t* iters;
   const int* in_list;
-  int* in_count;
+  const int* in_count;
   KParams P;
 };
 
@@ -773,48 +785,19 @@ template <int NV>
 __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGPR_ATTR void cmpc_solve_w_kernel(
     WideArgs A) {
   __shared__ SharedW<NV> sh;
-#if CMPC_WIDE_PERSIST
-  __shared__ int s_next;
-  for (;;) {
-    // every argument re-read per instance through an opaque pointer: hoisted out of the loop
-    // they would hold ~45 SGPRs for the whole kernel and spill
-    const WideArgs* a = &A;
-    asm volatile("" : "+s"(a));
-    if (threadIdx.x == 0) s_next = atomicSub(a->in_count, 1) - 1;  // consumes the list length
-    __syncthreads();
-    const int b = s_next;
-    if (b < 0) break;
-    const int inst = a->in_list[b];
-    solve_w<NV>(a->recs + (size_t)inst * a->P.rec_words, a->P, sh,
-                a->forces + (size_t)inst * 12 * a->P.N, a->status + inst,
-                a->iters ? a->iters + inst : nullptr);
-    __syncthreads();  // sh and s_next are free again
-  }
-#else
   const int b = blockIdx.x;
   if (b >= *A.in_count) return;
   const int inst = A.in_list[b];
   solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
               A.status + inst, A.iters ? A.iters + inst : nullptr);
-#endif
-}
-
-// workgroups of a persistent wide class: about two residency waves of the widest geometry
-inline int wide_grid(int list_bound) {
-#if CMPC_WIDE_PERSIST
-  return list_bound < 2048 ? list_bound : 2048;
-#else
-  return list_bound;
-#endif
 }
 
 template <int NV>
 hipError_t launch_wide_impl(const float* d_recs, const KParams& P, float* d_forces,
                             uint8_t* d_status, int32_t* d_iters, const int* in_list,
                             const int* in_count, int grid, hipStream_t stream) {
-  grid = wide_grid(grid);
   if (grid <= 0) return hipSuccess;
-  const WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, const_cast<int*>(in_count), P};
+  const WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, in_count, P};
   hipLaunchKernelGGL(cmpc_solve_w_kernel<NV>, dim3(grid), dim3(WGeo<NV>::NT), 0, stream, A);
   return hipGetLastError();
 }

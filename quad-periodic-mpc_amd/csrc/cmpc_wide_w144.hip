@@ -2,7 +2,7 @@
 // two waves per SIMD: at three the 72-column half rows spill (25 VGPRs); five waves per
 // workgroup, 52 KB of LDS
 #ifndef CMPC_WIDE_WAVES_PER_EU
-#define CMPC_WIDE_WAVES_PER_EU 2
+#define CMPC_WIDE_WAVES_PER_EU 3
 #endif
 #include "cmpc_wide.h"
 

@@ -152,6 +152,18 @@ class ShardedSolver:
             self._solver = None
 
 
+# Smallest pipeline piece worth cutting: below ~16384 instances a solve no longer fills the GPU's
+# 4096 class-1 wave slots several times over and the per-instance rate drops.
+MIN_PIECE = 16384
+MAX_CHUNKS = 4
+
+
+def auto_chunks(local_batch: int, min_piece: int = MIN_PIECE, max_chunks: int = MAX_CHUNKS) -> int:
+    """Pieces per rank for the config-4 pipeline: as many as keep every piece >= ``min_piece``
+    instances, at most ``max_chunks`` (262144 over 1 / 2 / 4 / 8 ranks -> 4 / 4 / 4 / 2)."""
+    return max(1, min(max_chunks, local_batch // max(1, min_piece)))
+
+
 def _chunk_plan(batch: int, world: int, chunks: int):
     """Per rank r and chunk c: rows [a_rc, b_rc) of the global batch (contiguous rank shards,
     each split into ``chunks`` contiguous pieces) and S_c = the largest piece c over ranks (the
@@ -170,10 +182,10 @@ class RootPipeline:
     one :meth:`step` scatters them over the ranks (RCCL over xGMI under the ``nccl`` backend),
     solves every rank's contiguous shard on its own GPU and gathers the forces back to root.
 
-    The shard of every rank is cut into ``chunks`` pieces and the three stages are software-
-    pipelined: the collectives run on the process group's communication stream, the solve on the
-    caller's current stream, so piece c+1 is in flight over xGMI while piece c is being solved
-    and piece c-1 is being gathered. Issue order per step (communication stream):
+    The shard of every rank is cut into ``chunks`` pieces (default :func:`auto_chunks`) and the
+    three stages are software-pipelined: the collectives run on the process group's
+    communication stream, the solve on the caller's current stream, so piece c+1 is in flight
+    over xGMI while piece c is being solved and piece c-1 is being gathered. Issue order per step (communication stream):
     scatter 0, scatter 1, gather 0, scatter 2, gather 1, ... — a gather never delays the next
     piece's scatter.
 
@@ -181,8 +193,8 @@ class RootPipeline:
     the default binds a :class:`BatchSolver` to the current stream. Every buffer is allocated
     here, none inside :meth:`step`."""
 
-    def __init__(self, params, global_batch: int, chunks: int = 4, *, group=None, device=None,
-                 src: int = 0, solve_fn=None, record_words: Optional[int] = None):
+    def __init__(self, params, global_batch: int, chunks: Optional[int] = None, *, group=None,
+                 device=None, src: int = 0, solve_fn=None, record_words: Optional[int] = None):
         from .records import record_words as _rw
         self.params = params
         self.N = params.horizon
@@ -191,6 +203,8 @@ class RootPipeline:
         self.group = group
         self.src = src
         self.world, self.rank = _group_info(group)
+        if chunks is None:   # adaptive: pieces of >= MIN_PIECE instances (auto_chunks)
+            chunks = auto_chunks(max(shard_sizes(self.batch, self.world)))
         self.chunks = max(1, min(int(chunks), max(1, self.batch // max(1, self.world))))
         self.plan, self.sizes = _chunk_plan(self.batch, self.world, self.chunks)
         self.start, self.stop = shard_bounds(self.batch, self.world, self.rank)

@@ -312,7 +312,29 @@ class BatchSolver:
         CI [B,n,m], ci0 [B,m]; optional per-instance ``dims`` [B,3] int32 (n, p, m)."""
         if batch is None:
             batch = G.shape[0]
+        batch = int(batch)
         n, p, m = int(G.shape[-1]), int(ce0.shape[-1]), int(ci0.shape[-1])
+        # (the QuadProg++ kernel keeps its state in LDS: batch is not bounded by max_batch)
+        # the kernel reads / writes these blocks through raw pointers: check dtype, layout and
+        # that every buffer holds `batch` instances before handing them over
+        import torch
+        shapes = {"G": (G, (n, n), torch.float64), "g0": (g0, (n,), torch.float64),
+                  "CE": (CE, (n, p), torch.float64), "ce0": (ce0, (p,), torch.float64),
+                  "CI": (CI, (n, m), torch.float64), "ci0": (ci0, (m,), torch.float64),
+                  "x": (x, (n,), torch.float64), "f": (f, (), torch.float64),
+                  "status": (status, (), torch.uint8)}
+        if iters is not None:
+            shapes["iters"] = (iters, (), torch.int32)
+        if dims is not None:
+            shapes["dims"] = (dims, (3,), torch.int32)
+        for name, (t, tail, dt) in shapes.items():
+            if t.dtype != dt:
+                raise CmpcError(f"quadprog: {name} must be {dt}, got {t.dtype}")
+            if not t.is_contiguous():
+                raise CmpcError(f"quadprog: {name} must be contiguous")
+            if t.dim() != 1 + len(tail) or tuple(t.shape[1:]) != tail or t.shape[0] < batch:
+                raise CmpcError(f"quadprog: {name} has shape {tuple(t.shape)}, expected "
+                                f"[>= {batch}, {', '.join(map(str, tail))}]")
         _check(self.lib.cmpc_batch_quadprog(self._h, n, p, m, _ptr(dims), _ptr(G), _ptr(g0),
                                             _ptr(CE), _ptr(ce0), _ptr(CI), _ptr(ci0), int(max_iter),
                                             _ptr(x), _ptr(f), _ptr(status), _ptr(iters), int(batch)),

@@ -157,4 +157,4 @@ def test_config5_full_size_sampled_live_reference(cm, orc, solver_mod, on_stream
     assert (np.abs(fe_dev - fe_ref) / np.maximum(np.abs(fe_ref), 1.0)).max() <= 1e-5
     ok = st_ref == 0
     assert ok.mean() > 0.99
-    assert_parity(orc, rec_s, prm, forces.cpu().numpy()[idx], q_ref, ok)
+    assert_parity(orc, rec_s, prm, forces.cpu().numpy()[idx], q_ref, ok, label="config 5 sampled")

@@ -5,13 +5,15 @@ reference pipeline run live on the same seeded inputs.
 Tolerance (north_star): ground-reaction forces within 1e-4 relative to qpOASES, norm-wise per
 instance: |f - f_ref|_inf / max(|f_ref|_inf, 1 N) <= 1e-4 at every horizon, N = 20 included.
 
-At N >= 16 the reference's own fp32 pipeline is itself up to ~1e-4 away from the optimum of the
+N <= 16 (the deployed horizon, ros_config.yaml:93) is held to that bound on every instance.
+At N >= 17 the reference's own fp32 pipeline is itself up to ~1e-4 away from the optimum of the
 QP it approximates (scripts/exact_gap.py: 9.97e-5 on the live N = 20 set below, cond(H) ~ 3e3),
 so two correct fp32 implementations can differ by up to twice that. There, an instance that
 misses 1e-4 against qpOASES still passes if it is within 1e-4 of the float64 optimum of the same
 reference pipeline (oracle.fp64_solve: fp64 expm, condensation and qpOASES) — i.e. it is at least
 as accurate as north_star asks, measured against the exact answer rather than against the
-reference's rounding. Every such instance is counted and capped (<= 2 % of a batch).
+reference's rounding. Every such instance is counted, printed with its errors, and capped
+(<= 2 % of a batch).
 """
 import importlib
 
@@ -27,20 +29,30 @@ def tol_for(N):
     return 1e-4
 
 
-def assert_parity(orc, recs, prm, f, q_ref, ok=None):
-    """err vs qpOASES <= 1e-4, or (N >= 16 only) err vs the fp64 optimum <= 1e-4 (module doc)."""
+FP64_BRANCH_MIN_N = 17   # below this every instance is held to 1e-4 against qpOASES
+
+
+def assert_parity(orc, recs, prm, f, q_ref, ok=None, label=""):
+    """err vs qpOASES <= 1e-4; at N >= 17 only, err vs the fp64 optimum <= 1e-4 instead, for at
+    most 2 % of the batch (module doc). Prints how many instances took that branch."""
     ok = np.ones(len(q_ref), bool) if ok is None else ok
     err = rel_force_err(f[ok], q_ref[ok])
     bad = np.nonzero(err > tol_for(prm.horizon))[0]
-    if len(bad) and prm.horizon >= 16:
-        assert len(bad) <= max(1, int(0.02 * len(err))), (len(bad), err.max())
+    msg = (f"[parity] {label} N={prm.horizon}: {len(err)} instances, max err vs qpOASES "
+           f"{err.max():.2e}, {len(bad)} beyond {tol_for(prm.horizon):.0e}")
+    if len(bad) and prm.horizon >= FP64_BRANCH_MIN_N:
         idx = np.nonzero(ok)[0][bad]
+        e64s = []
         for i in idx:
             x64, ri = orc.fp64_solve(recs[i], prm)
             assert ri == 0
-            e64 = np.abs(f[i] - x64).max() / max(np.abs(x64).max(), 1.0)
-            assert e64 <= tol_for(prm.horizon), (int(i), err.max(), e64)
+            e64s.append(np.abs(f[i] - x64).max() / max(np.abs(x64).max(), 1.0))
+        print(msg + f" -> fp64-optimum branch: worst vs qpOASES {err[bad].max():.2e}, "
+              f"worst vs fp64 optimum {max(e64s):.2e}")
+        assert len(bad) <= max(1, int(0.02 * len(err))), (len(bad), err.max())
+        assert max(e64s) <= tol_for(prm.horizon), (err.max(), max(e64s))
         return
+    print(msg)
     assert len(bad) == 0, (err.max(), int(np.argmax(err)))
 
 
@@ -112,7 +124,7 @@ def test_random_batches_match_reference_live(cm, orc, solver_mod, N, stress, fra
     f, st, it = gpu_solve(solver_mod, prm, recs)
     ok = st_ref == 0
     assert (st[ok] == 0).all()
-    assert_parity(orc, recs, prm, f, q, ok)
+    assert_parity(orc, recs, prm, f, q, ok, label=f"live stress={stress} frac={frac}")
 
 
 def test_device_path_deterministic(cm, solver_mod):

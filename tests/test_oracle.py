@@ -186,7 +186,7 @@ def test_config5_golden_self_consistent(cm, orc):
 
 
 def test_fp64_pipeline_close_to_reference(cm, orc):
-    """oracle.fp64_solve (the float64 optimum the parity rule at N >= 16 falls back to) agrees
+    """oracle.fp64_solve (the float64 optimum the parity rule at N >= 17 falls back to) agrees
     with the reference fp32 pipeline to the reference's own rounding: <= 2e-5 at N = 10 and
     <= 1.5e-4 at N = 20 (scripts/exact_gap.py)."""
     if not orc.ref_available():
