@@ -54,6 +54,27 @@ def test_root_pipeline_world1_bitwise_and_parity(cm, orc, config4):
     prm, recs, solver_mod = config4
     par = importlib.import_module("quad-periodic-mpc_amd.parallel")
     recs_dev = torch.from_numpy(recs).cuda()
+    # the pipeline launches on the caller's current stream, which must not be the null stream
+    # (as bench.py does: one non-default stream per rank)
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        f_pipe, st_pipe = _pipeline_world1(par, prm, recs_dev)
+    torch.cuda.synchronize()
+    assert (st_pipe == 0).all(), np.bincount(st_pipe)
+    f_one, st_one = _one_launch(solver_mod, prm, recs_dev)
+    assert (st_one == 0).all()
+    np.testing.assert_array_equal(f_pipe, f_one)
+    if orc.ref_available():
+        idx = np.random.default_rng(4).choice(BATCH, 512, replace=False)
+        q, st_ref, _ = orc.ref_solve_batch(recs[idx], prm, nthreads=16)
+        ok = st_ref == 0
+        err = rel_force_err(f_pipe[idx][ok], q[ok])
+        print(f"[config4] 512 sampled of {BATCH}: max rel err vs qpOASES {err.max():.2e}")
+        assert err.max() <= 1e-4
+
+
+def _pipeline_world1(par, prm, recs_dev):
     pipe = par.RootPipeline(prm, BATCH, chunks=4, device="cuda")
     try:
         assert pipe.chunks == 4 and pipe.sizes == [BATCH // 4] * 4
@@ -67,17 +88,7 @@ def test_root_pipeline_world1_bitwise_and_parity(cm, orc, config4):
         np.testing.assert_array_equal(pipe.forces.cpu().numpy(), f_pipe)
     finally:
         pipe.close()
-    assert (st_pipe == 0).all(), np.bincount(st_pipe)
-    f_one, st_one = _one_launch(solver_mod, prm, recs_dev)
-    assert (st_one == 0).all()
-    np.testing.assert_array_equal(f_pipe, f_one)
-    if orc.ref_available():
-        idx = np.random.default_rng(4).choice(BATCH, 512, replace=False)
-        q, st_ref, _ = orc.ref_solve_batch(recs[idx], prm, nthreads=16)
-        ok = st_ref == 0
-        err = rel_force_err(f_pipe[idx][ok], q[ok])
-        print(f"[config4] 512 sampled of {BATCH}: max rel err vs qpOASES {err.max():.2e}")
-        assert err.max() <= 1e-4
+    return f_pipe, st_pipe
 
 
 def _free_port():
