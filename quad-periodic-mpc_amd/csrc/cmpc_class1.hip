@@ -22,6 +22,8 @@
 //   * every loop over matrix columns is unrolled at compile time, so register indices are
 //     constants; LDS traffic between lanes of the single wavefront needs no s_barrier.
 // Everything is fp32 (the reference condenses in fp32: common_types.h:14).
+#include <stdlib.h>
+
 #include "cmpc_common.h"
 
 #ifndef CMPC_W1_WAVES_PER_EU
@@ -32,21 +34,43 @@
 #ifndef CMPC_C1_RL
 #define CMPC_C1_RL 0
 #endif
+// Cholesky two pivots per step (rank-2 sweeps); 0: one pivot per step
+#ifndef CMPC_C1_CHOL2
+#define CMPC_C1_CHOL2 1
+#endif
 
 // Phase profiler (diagnostic builds only, -DCMPC_PHASE_PROF): lane 0 of every solved instance
 // adds the s_memtime cycles spent in each stage to g_c1_phase (scripts/phase_prof.py).
 #ifdef CMPC_PHASE_PROF
-__device__ unsigned long long g_c1_phase[8];
+__device__ unsigned long long g_c1_phase[16];
 #define C1_MARK(i)                              \
   do {                                          \
     const unsigned long long _n = clock64();    \
     ph[i] += _n - t_last;                       \
     t_last = _n;                                \
   } while (0)
+// active-set loop segments [8 + i], timed from the top of the trip
+#define C1_SUB(i)                               \
+  do {                                          \
+    const unsigned long long _n = clock64();    \
+    ph[8 + (i)] += _n - t_sub;                  \
+    t_sub = _n;                                 \
+  } while (0)
 #else
 #define C1_MARK(i) \
   do {             \
   } while (0)
+#define C1_SUB(i) \
+  do {            \
+  } while (0)
+#endif
+
+// Placement profiler (diagnostic builds only, -DCMPC_PLACE_PROF): per instance the hardware
+// wave id, the XCC id and the wall-clock (100 MHz) start / end of its wavefront
+// (scripts/place_prof.py).
+#ifdef CMPC_PLACE_PROF
+constexpr int kPlaceMax = 65536;
+__device__ unsigned int g_c1_place[4 * kPlaceMax];
 #endif
 
 namespace cmpc {
@@ -145,7 +169,8 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   const int v = threadIdx.x;
   const int N = P.N;
 #ifdef CMPC_PHASE_PROF
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_sub = 0;
   unsigned long long t_last = clock64();
 #endif
   // ---- stage the record in LDS: one 16-B load per lane, so the whole prep waits on a single
@@ -267,17 +292,12 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 #pragma unroll
       for (int j = 0; j < 13; j++) gk[j] = act ? fmaf(k2, u2[j], fmaf(k, u1[j], b[j])) : 0.f;
       recur(md, wts, gk, z);
+      asm volatile("" ::: "memory");  // the Bdt column loads stay inside the step
       const int wb = __builtin_amdgcn_readfirstlane(sh.blkbase[i]);
-      const int we = __builtin_amdgcn_readfirstlane(sh.blkbase[i + 1]);
-      for (int w = wb; w < we; w++) {
-        const int cw = sh.varcol[w];
-        float bw[13];
-#pragma unroll
-        for (int j = 0; j < 13; j++) bw[j] = sh.u.BdtT[cw][j];
-        float val = 2.f * dot13(bw, z);
+      step_columns(sh.u.BdtT, step_mask(msk0, msk1, i), wb, z, [&](int w, float val) {
         if (w == v) val += P.alpha2;  // qH = 2 (B'SB + alpha I), SolverMPC.cpp:806
         if (act && w >= v) sh.P[myrow + w] = val;
-      }
+      });
     }
   }
   lsync();
@@ -309,6 +329,70 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   // bound). The stored columns also feed J = L^-T below.
   int status = CMPC_OK;
   float my_inv = 1.f;
+#if CMPC_C1_CHOL2
+  // Two pivots per step (k even, k+1): one rank-2 sweep over the raw column k and column k+1
+  // as it is after step k,
+  //   slot[c] += a0 P_k[c] + a1 P_k+1[c]  (c >= k+2),  a0 = -H[v][k] / d_k,  a1 = -s1 / d_k+1,
+  //   s1 = H[v][k+1] - beta H[v][k],  beta = H[k+1][k] / d_k,  d_k+1 = H[k+1][k+1] - beta H[k+1][k]
+  // so the 60 serial steps (pivot, broadcast, LDS round trip) become 30 with the same FMA count.
+  // Look-ahead: as soon as the sweep chunk holding columns k+2, k+3 is updated, the step takes
+  // their pivot data by readlane, forms the next step's beta / d / 1/sqrt(d), and publishes
+  // column k+2 and the corrected column k+3; so the next step starts on its sweep at once. The
+  // stored columns (raw even, corrected odd) are what J = L^-T needs. Odd n: the last step's
+  // second pivot is the identity padding row (H[n][n] = 1, no coupling).
+  float i0n = 1.f, betan = 0.f, i1n = 1.f, g0n = 0.f, g1n = 0.f;
+  // pivot data of the step at columns (j, j+1) from the current rows, and the publish of both
+  // columns (lanes >= the columns' chunk start)
+  auto look = [&](auto JJ) {
+    constexpr int j = decltype(JJ)::value, j1 = j + 1;
+    constexpr int cj = j & ~3, cj1 = j1 & ~3;
+    if constexpr (j1 < NV) {  // (also instantiated, never called, past the last step)
+    float d0 = rl(slot[j], j);
+    const float h10 = rl(slot[j], j1);
+    if (!(d0 > 0.f)) { status = CMPC_NOT_PD; d0 = 1e-30f; }
+    i0n = __builtin_amdgcn_rsqf(d0);  // d is a normal positive pivot
+    betan = h10 * (i0n * i0n);
+    float d1 = fmaf(-h10, betan, rl(slot[j1], j1));
+    if (!(d1 > 0.f)) { status = CMPC_NOT_PD; d1 = 1e-30f; }
+    i1n = __builtin_amdgcn_rsqf(d1);
+    g0n = rl(slot[NV], j);
+    g1n = fmaf(-betan, g0n, rl(slot[NV], j1));  // border of row j+1 after step j
+    const float s1 = fmaf(-slot[j], betan, slot[j1]);
+    if (v >= cj && v < NV) sh.P[G::prow(j) + v - cj] = (v >= j) ? slot[j] : 0.f;
+    if (v >= cj1 && v < NV) sh.P[G::prow(j1) + v - cj1] = (v >= j1) ? s1 : 0.f;
+    lsync();
+    }
+  };
+  if (n > 0) look(std::integral_constant<int, 0>{});
+  static_for<0, NV / 2>([&](auto KB) {
+    constexpr int k = 2 * decltype(KB)::value;
+    constexpr int k1 = k + 1, k2 = k + 2;
+    constexpr int c0 = k & ~3, c1 = k1 & ~3, c2 = k2 & ~3;
+    constexpr int rk = G::prow(k), rk1 = G::prow(k1);
+    if (k < n) {
+      const float i0 = i0n, beta = betan, i1 = i1n, g0 = g0n, g1 = g1n;
+      if (v == k) { my_inv = i0; sh.u.ibuf[k] = i0; }
+      if (v == k1) { my_inv = i1; sh.u.ibuf[k1] = i1; }
+      const float s0 = slot[k];
+      const float s1 = fmaf(-s0, beta, slot[k1]);
+      const float a0 = (v > k) ? -s0 * (i0 * i0) : 0.f;
+      const float a1 = (v > k1) ? -s1 * (i1 * i1) : 0.f;
+      slot[NV] = fmaf(a1, g1, fmaf(a0, g0, slot[NV]));
+      static_for<c2 / 4, NV / 4>([&](auto JC) {
+        constexpr int c = 4 * decltype(JC)::value;
+        const float4 r0 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
+        const float4 r1 = *reinterpret_cast<const float4*>(&sh.P[rk1 + c - c1]);
+        axpy4(a0, r0, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
+        axpy4(a1, r1, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
+        if constexpr (k2 < NV && c == c2) {
+          if (k2 < n) look(std::integral_constant<int, k2>{});  // columns k+2, k+3 are final
+        }
+        CMPC_SWEEP_FENCE(c);
+      });
+      pin(slot);
+    }
+  });
+#else
   float dnext = 1.f, gnext = 0.f;
   if (n > 0) {
     if (v < NV) sh.P[G::prow(0) + v] = slot[0];
@@ -364,6 +448,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       pin(slot);
     }
   });
+#endif
   const float yv = (v < n) ? slot[NV] * my_inv : 0.f;  // L y = g
   lsync();
   C1_MARK(2);
@@ -373,6 +458,34 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     constexpr int c = decltype(C)::value;
     slot[c] = (c == v) ? 1.f : 0.f;
   });
+#if CMPC_C1_CHOL2
+  // two columns per step, as the factorisation: x_k, then x_k+1 after column k's term, then one
+  // rank-2 sweep over the stored columns k, k+1 (the odd-n padding column is the identity)
+  static_for<0, NV / 2>([&](auto KB) {
+    constexpr int k = 2 * decltype(KB)::value;
+    constexpr int k1 = k + 1, c2 = (k + 2) & ~3;
+    constexpr int c0 = k & ~3, c1 = k1 & ~3;
+    constexpr int rk = G::prow(k), rk1 = G::prow(k1);
+    if (k < n) {  // P and ibuf are read-only here: no per-step LDS ordering needed
+      const float i0 = sh.u.ibuf[k], i1 = sh.u.ibuf[k1];
+      const float h = sh.P[rk + k1 - c0];  // L[k+1][k] sqrt(d_k)
+      const float x0 = slot[k] * i0;
+      const float x1 = fmaf(-h * i0, x0, slot[k1]) * i1;
+      const float a0 = -x0 * i0, a1 = -x1 * i1;
+#pragma unroll
+      for (int c = c2; c < NV; c += 4) {
+        const float4 r0 = *reinterpret_cast<const float4*>(&sh.P[rk + c - c0]);
+        const float4 r1 = *reinterpret_cast<const float4*>(&sh.P[rk1 + c - c1]);
+        axpy4(a0, r0, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
+        axpy4(a1, r1, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
+        CMPC_SWEEP_FENCE(c);
+      }
+      slot[k] = x0;
+      slot[k1] = x1;
+      pin(slot);
+    }
+  });
+#else
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int c0 = k & ~3;
@@ -391,6 +504,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       pin(slot);
     }
   });
+#endif
 
   C1_MARK(3);
   // ---- unconstrained minimiser x = -J y ----------------------------------------------------
@@ -427,6 +541,9 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     for (;;) {
       pin(slot);
       const int v = tid_opq();  // re-materialised: keeps per-lane addresses out of the preheader
+#ifdef CMPC_PHASE_PROF
+      t_sub = clock64();
+#endif
       if (p < 0) {
         sh.u.gi.xs[v] = xv;
         lsync();
@@ -453,6 +570,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         cp = decode_cons(p, mui, sh.sub[p / 6]);
         up = 0.f;
       }
+      C1_SUB(0);
       if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
       // d = J' n+ : rows ia, iz of J through LDS (dword stores: wide stores would tie the row
       // registers into tuples)
@@ -483,13 +601,28 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       // and the NV loaded values of vbuf stay live across it (158 VGPRs, three waves per SIMD)
       asm volatile("" : "+v"(zv), "+v"(zn));
       const float dn = wave_sum((v < n) ? dv * dv : 0.f);
+      C1_SUB(1);
       // r = R^-1 d1: back substitution over the packed columns of R (lane i ends with r_i)
+      // (software-pipelined: the LDS reads of step i - 1 are issued before step i's chain)
       float acc = dv, r_reg = 0.f;
-      for (int i = q - 1; i >= 0; i--) {
-        const int off = rcol(i);
-        const float ri = fdiv(rl(acc, i), sh.P[off + i]);
-        if (v < i) acc = fmaf(-sh.P[off + v], ri, acc);
-        r_reg = (v == i) ? ri : r_reg;
+      {
+        float pd = 1.f, pv = 0.f;
+        if (q > 0) {
+          pd = sh.P[rcol(q - 1) + q - 1];
+          pv = sh.P[rcol(q - 1) + v];
+        }
+        for (int i = q - 1; i >= 0; i--) {
+          float pd_n = 1.f, pv_n = 0.f;
+          if (i > 0) {
+            pd_n = sh.P[rcol(i - 1) + i - 1];
+            pv_n = sh.P[rcol(i - 1) + v];
+          }
+          const float ri = fdiv(rl(acc, i), pd);
+          if (v < i) acc = fmaf(-pv, ri, acc);
+          r_reg = (v == i) ? ri : r_reg;
+          pd = pd_n;
+          pv = pv_n;
+        }
       }
       // partial (dual) step t1, full (primal) step t2
       float t1 = kBigF;
@@ -504,7 +637,9 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       if (v < q) u_reg = fmaf(-t, r_reg, u_reg);
       up += t;
       if (!zero_step) xv = fmaf(t, zv, xv);
+      C1_SUB(2);
       const bool add = !zero_step && t2 <= t1;
+      const bool add_u = __builtin_amdgcn_readfirstlane((int)add) != 0;
       float beta = 0.f;
       if (add) {
         // ---- add p: the Householder reflection I - beta w w' on columns q..n-1 maps
@@ -514,7 +649,6 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         const float sgn = (dq >= 0.f) ? 1.f : -1.f;
         beta = fast_rcp(ts * (ts + fabsf(dq)));  // 2 / (w'w)
         sh.vbuf[v] = (v == q) ? dq + sgn * ts : dm;
-        *reinterpret_cast<float2*>(&sh.u.gi.cs[2 * v]) = make_float2(1.f, 0.f);
         const int offq = rcol(q);
         if (v < q) sh.P[offq + v] = dv;
         if (v == q) {
@@ -561,8 +695,10 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         }
       }
       lsync();
-      // Both J updates run as straight-line code on every trip (a uniform add/drop branch here
-      // makes the allocator duplicate the row: 224-256 VGPRs instead of 166).
+      C1_SUB(3);
+      // The reflection runs on every trip (beta = 0 on a drop: a uniform branch around it costs 27
+      // spilled VGPRs); the Givens chain only on a drop (add_u is wave-uniform; the branch leaves
+      // the register allocation unchanged, same instruction count).
       {
         // J <- J (I - beta w w'): tw = J_v . w, J_v -= beta tw w  (no-op on a drop: beta = 0)
         f2v tacc = {0.f, 0.f};
@@ -583,8 +719,9 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           CMPC_SWEEP_FENCE(c);
         }
       }
-      {
-        // J columns (j, j+1) <- Givens chain j = 0 .. NV-2 (identity on an add)
+      C1_SUB(4);
+      if (!add_u) {
+        // J columns (j, j+1) <- Givens chain j = 0 .. NV-2 (drops only)
         static_for<0, NV - 1>([&](auto JC) {
           constexpr int j = decltype(JC)::value;
           const float2 cs2 = *reinterpret_cast<const float2*>(&sh.u.gi.cs[2 * j]);
@@ -594,6 +731,10 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
         });
       }
+      C1_SUB(5);
+#ifdef CMPC_PHASE_PROF
+      ph[14] += add ? 0ull : 1ull;
+#endif
       if (add) {
         q++;
         p = -1;
@@ -623,7 +764,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     ph[6] = 1;
     ph[7] = (unsigned long long)iters;
 #pragma unroll
-    for (int i = 0; i < 8; i++) atomicAdd(&g_c1_phase[i], ph[i]);
+    for (int i = 0; i < 16; i++) atomicAdd(&g_c1_phase[i], ph[i]);
   }
 #endif
 }
@@ -645,19 +786,39 @@ __global__ __launch_bounds__(64, CMPC_W1_WAVES_PER_EU) void cmpc_solve_c1_kernel
   } else if (t >= batch) {
     return;
   }
+#ifdef CMPC_PLACE_PROF
+  const unsigned long long t_start = wall_clock64();
+  const unsigned hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+  const unsigned xcc_id = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+#endif
   solve_c1<NV>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * 12 * P.N, status + t,
                iters ? iters + t : nullptr, ovf_list, ovf_count, t);
+#ifdef CMPC_PLACE_PROF
+  const unsigned long long t_end = wall_clock64();
+  if (threadIdx.x == 0 && t < kPlaceMax) {
+    g_c1_place[4 * t + 0] = hw_id;
+    g_c1_place[4 * t + 1] = xcc_id;
+    g_c1_place[4 * t + 2] = (unsigned)t_start;
+    g_c1_place[4 * t + 3] = (unsigned)t_end;
+  }
+#endif
 }
 
 hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream) {
   if (grid <= 0) return hipSuccess;
+  // CMPC_C1_DYN_LDS=<bytes> (diagnostic): extra dynamic LDS per workgroup, i.e. fewer class-1
+  // workgroups per CU (placement / occupancy experiments)
+  static const unsigned dyn = [] {
+    const char* e = getenv("CMPC_C1_DYN_LDS");
+    return e ? (unsigned)atoi(e) : 0u;
+  }();
   if (nv == 60)
-    hipLaunchKernelGGL(cmpc_solve_c1_kernel<60>, dim3(grid), dim3(64), 0, stream, d_recs, batch, P,
+    hipLaunchKernelGGL(cmpc_solve_c1_kernel<60>, dim3(grid), dim3(64), dyn, stream, d_recs, batch, P,
                        d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
   else
-    hipLaunchKernelGGL(cmpc_solve_c1_kernel<64>, dim3(grid), dim3(64), 0, stream, d_recs, batch, P,
+    hipLaunchKernelGGL(cmpc_solve_c1_kernel<64>, dim3(grid), dim3(64), dyn, stream, d_recs, batch, P,
                        d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);
   return hipGetLastError();
 }
@@ -668,9 +829,17 @@ hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& 
 // cycles per stage summed over solved class-1 instances: prep, condensation, Cholesky, J,
 // active set (incl. x = -J y), scatter; [6] instances, [7] active-set iterations. Resets.
 extern "C" int cmpc_debug_phase_read(unsigned long long* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c1_phase), sizeof(unsigned long long) * 8) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c1_phase), sizeof(unsigned long long) * 16) != hipSuccess)
     return -1;
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long z[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_c1_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef CMPC_PLACE_PROF
+// per instance [hw_id, xcc_id, start, end] of the last class-1 launches (instances < 65536)
+extern "C" int cmpc_debug_place_read(unsigned int* out, int n) {
+  if (n > kPlaceMax) n = kPlaceMax;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c1_place), sizeof(unsigned int) * 4 * n) == hipSuccess ? 0 : -1;
 }
 #endif

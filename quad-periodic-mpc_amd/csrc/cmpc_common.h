@@ -206,6 +206,40 @@ __device__ __forceinline__ float dot13(const float* a, const float* b) {
   return s;
 }
 
+// stance mask of horizon step i (bit f: foot f in stance) from the two stance ballots over the
+// foot-steps 4 i + f (m0: foot-steps 0..63, m1: 64..127); uniform
+__device__ __forceinline__ unsigned step_mask(unsigned long long m0, unsigned long long m1, int i) {
+  return (unsigned)(((i < 16) ? (m0 >> (4 * i)) : (m1 >> (4 * i - 64))) & 15ull);
+}
+
+// The H entries of horizon step i for one row: for every stance foot f of the step (uniform
+// mask mi, ascending) and axis a, column c = 3 f + a of Bdt lands at reduced column
+// w = wb + 3 rank(f) + a with value 2 b_c' z. Unrolled over the 4 feet x 3 axes with uniform
+// branches: the Bdt columns are broadcast LDS reads at constant addresses, with no
+// column-id -> column dependent-load chain (the dynamic loop over the step's columns waited on
+// two LDS round trips per column). st(w, val) stores the entry.
+template <class St>
+__device__ __forceinline__ void step_columns(const float (*BdtT)[16], unsigned mi, int wb,
+                                             const float* z, St&& st) {
+  int w = wb;
+  static_for<0, 4>([&](auto F) {
+    constexpr int f = decltype(F)::value;
+    if (mi & (1u << f)) {
+      static_for<0, 3>([&](auto A) {
+        constexpr int c = 3 * f + decltype(A)::value;
+        float bw[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const float4 b4 = *reinterpret_cast<const float4*>(&BdtT[c][4 * q]);
+          bw[4 * q] = b4.x; bw[4 * q + 1] = b4.y; bw[4 * q + 2] = b4.z; bw[4 * q + 3] = b4.w;
+        }
+        st(w, 2.f * dot13(bw, z));
+        w++;
+      });
+    }
+  });
+}
+
 // quaternion (w,x,y,z) -> rotation matrix, as Eigen's toRotationMatrix (RobotState.cpp:36)
 __device__ __forceinline__ void make_model(const float* __restrict__ rec, float dt, Model& md) {
   const float qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],

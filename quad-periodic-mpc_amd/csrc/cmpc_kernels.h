@@ -35,7 +35,8 @@ struct LocoParams {
 // 128, 192, 256 columns, general), [8 ..) the six lists of max_batch entries each
 // instance lists of the classify pass: 80, 96, 128, 192, 256, G, 144, and 7: class-1 instances
 // with 60 < n <= 64 (the 64-wide class-1 build; n <= 60 runs in the 60-wide build over the
-// whole batch). d_work = [kHdr ints: cnt[0] total, cnt[1 + list]] [kLists lists of max_batch]
+// whole batch). d_work = [kHdr ints: cnt[0] total, cnt[1 + list] list lengths, cnt[9 + list] the
+// persistent wide workgroups' dequeue counters] [kLists lists of max_batch]
 constexpr int kLists = 8;
 constexpr int kHdr = 16;
 inline size_t work_ints(int max_batch) { return kHdr + kLists * (size_t)max_batch; }
@@ -67,7 +68,7 @@ hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& 
 #define CMPC_DECL_WIDE(W)                                                                          \
   hipError_t launch_wide_w##W(const float* d_recs, const KParams& P, float* d_forces,             \
                               uint8_t* d_status, int32_t* d_iters, const int* in_list,            \
-                              const int* in_count, int grid, hipStream_t stream);
+                              const int* in_count, int* deq, int grid, hipStream_t stream);
 CMPC_DECL_WIDE(80)
 CMPC_DECL_WIDE(96)
 CMPC_DECL_WIDE(128)

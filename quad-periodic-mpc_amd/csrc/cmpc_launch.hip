@@ -111,23 +111,33 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       return e;
     // side 0: 80, 128, 256; side 1: 96, 144, 192 (at N = 20 the 128-column class and the
     // 144/192-column classes, which carry the batch, run side by side)
-    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], grid_of[0],
+    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], &cnt[9 + 0], grid_of[0],
                              ctx.side[0])) != hipSuccess)
       return e;
-    if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2],
+    if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], &cnt[9 + 1],
                                            grid_of[1], ctx.side[1])) != hipSuccess)
       return e;
-    if (n_max > 96 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
+    // CMPC_WIDE_ORDER=1 (A/B): the 144 class ahead of the 128 class on side 0 (longest solves
+    // first, no concurrent 128-class workgroups to starve its dispatch)
+    static const int order = [] {
+      const char* v = getenv("CMPC_WIDE_ORDER");
+      return v ? atoi(v) : 0;
+    }();
+    if (order == 1 && n_max > 128 &&
+        (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], &cnt[9 + 6], grid_of[6],
+                              ctx.side[0])) != hipSuccess)
+      return e;
+    if (n_max > 96 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3], &cnt[9 + 2],
                                             grid_of[2], ctx.side[0])) != hipSuccess)
       return e;
-    if (n_max > 128 &&
-        (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], grid_of[6],
+    if (order != 1 && n_max > 128 &&
+        (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], &cnt[9 + 6], grid_of[6],
                               ctx.side[1])) != hipSuccess)
       return e;
-    if (n_max > 144 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4],
+    if (n_max > 144 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4], &cnt[9 + 3],
                                              grid_of[3], ctx.side[1])) != hipSuccess)
       return e;
-    if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5],
+    if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5], &cnt[9 + 4],
                                              grid_of[4], ctx.side[0])) != hipSuccess)
       return e;
     const bool g_possible = n_max > 256;
@@ -163,12 +173,12 @@ hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_f
   if (n <= 64)
     return launch_class1(n <= 60 ? 60 : 64, d_rec, 1, P, d_forces, d_status, d_iters, nullptr,
                          nullptr, nullptr, nullptr, 1, stream);
-  if (n <= 80) return launch_wide_w80(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
-  if (n <= 96) return launch_wide_w96(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
-  if (n <= 128) return launch_wide_w128(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
-  if (n <= 144) return launch_wide_w144(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
-  if (n <= 192) return launch_wide_w192(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
-  if (n <= 256) return launch_wide_w256(d_rec, P, d_forces, d_status, d_iters, lst, cnt, 1, stream);
+  if (n <= 80) return launch_wide_w80(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
+  if (n <= 96) return launch_wide_w96(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
+  if (n <= 128) return launch_wide_w128(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
+  if (n <= 144) return launch_wide_w144(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
+  if (n <= 192) return launch_wide_w192(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
+  if (n <= 256) return launch_wide_w256(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
   return launch_classg(d_rec, 1, P, d_forces, d_status, d_iters, lst, cnt, d_gscratch, 1, stream);
 }
 

@@ -36,6 +36,13 @@
 #define CMPC_WIDE_WAVES_PER_EU 3
 #endif
 // hard VGPR cap per row width (0: none); 128 = four waves per SIMD
+// Cholesky and J = L^-T two pivots per step (rank-2 sweeps, half the barriers); 0: one
+#ifndef CMPC_WIDE_CHOL2
+#define CMPC_WIDE_CHOL2 1
+#endif
+#ifndef CMPC_WIDE_J2
+#define CMPC_WIDE_J2 CMPC_WIDE_CHOL2
+#endif
 #ifndef CMPC_WIDE_VGPR_CAP
 #define CMPC_WIDE_VGPR_CAP 0
 #endif
@@ -75,6 +82,17 @@ struct WGeo {
   static constexpr int PSZ_R = NV * (NV + 1) / 2;
   static constexpr int mx(int a, int b) { return a > b ? a : b; }
   static constexpr int PSZ = mx(mx(PSZ_H, PSZ_F), PSZ_R);
+  // stage buffers behind P (offsets into SharedW::P). Prep + condensation: BdtT at PSZ;
+  // Cholesky, J, x = -J y: ibuf, gbuf, ybuf at PSZ; active set: vbuf, bufA, bufB, dfull, xs, cs
+  // from PSZ_R on (the factor rows are dead by then and R never reaches past PSZ_R). At NV = 128
+  // this is 39 KB in place of 43: four workgroups per CU instead of three
+  static constexpr int O_IBUF = PSZ, O_GBUF = PSZ + NV, O_YBUF = PSZ + 2 * NV;
+  static constexpr int CH = 2 * NV + 2 * (NH + 4);
+  static constexpr int O_VBUF = PSZ_R, O_BUFA = O_VBUF + VL, O_BUFB = O_BUFA + VL;
+  static constexpr int O_DFULL = O_BUFB + VL, O_XS = O_DFULL + NV, O_CS = O_XS + NV;
+  static constexpr int GI_END = O_CS + 2 * NV + 8;
+  static constexpr int PTOT = (mx(mx(PSZ + 12 * 16, PSZ + CH), GI_END) + 3) & ~3;
+  static_assert(PSZ % 4 == 0 && PSZ_R % 4 == 0 && VL % 4 == 0, "16-B aligned stage buffers");
 };
 
 // logical-order LDS index (half 1 starts HOFF words in: the halves' ds_read_b128 never share a bank)
@@ -91,16 +109,7 @@ constexpr int W_OFF_REC = W_OFF_ZE + 16 * MAXN;   // LDS copy of the instance re
 template <int NV>
 struct SharedW {
   using G = WGeo<NV>;
-  alignas(16) float P[G::PSZ];
-  float BdtT[12][16];
-  float ibuf[NV];             // 1 / sqrt(d_k) of pivot k
-  float gbuf[NV];             // gradient border of pivot row k
-  float ybuf[2][G::NH + 4];   // y = L^-1 g, de-interleaved: ybuf[h][j] = y[2 j + h]
-  float vbuf[G::VL];          // masked d, then the Householder vector (logical order)
-  float bufA[G::VL], bufB[G::VL];  // J rows ia, iz (logical order)
-  float dfull[NV];            // d = J' n+ (logical index)
-  float xs[NV];               // x by reduced variable
-  float cs[2 * NV + 8];       // Givens (c, s) per logical column pair (half 1 at +4 words)
+  alignas(16) float P[G::PTOT];  // H / factor / R, then the stage buffers (WGeo offsets)
   float redf[16];
   int redi[16];
   float sub[4 * MAXN];        // ub of each stance foot-step (gait * f_max)
@@ -109,6 +118,18 @@ struct SharedW {
   unsigned char varblk[G::NT], varcol[G::NT];
   unsigned char stance[4 * MAXN];
   unsigned char cflag[2 * NV + 8];  // active flag per constraint id (6 per stance foot-step)
+  int deq_b;                  // list entry dequeued by the workgroup (persistent launches)
+  __device__ __forceinline__ float (*BdtT())[16] { return reinterpret_cast<float(*)[16]>(&P[G::PSZ]); }
+  __device__ __forceinline__ float* ibuf() { return &P[G::O_IBUF]; }    // 1 / sqrt(d_k) of pivot k
+  __device__ __forceinline__ float* gbuf() { return &P[G::O_GBUF]; }    // gradient border of pivot row k
+  // y = L^-1 g, de-interleaved: ybuf(h)[j] = y[2 j + h]
+  __device__ __forceinline__ float* ybuf(int h) { return &P[G::O_YBUF + h * (G::NH + 4)]; }
+  __device__ __forceinline__ float* vbuf() { return &P[G::O_VBUF]; }    // masked d, then the Householder vector
+  __device__ __forceinline__ float* bufA() { return &P[G::O_BUFA]; }    // J rows ia, iz (logical order)
+  __device__ __forceinline__ float* bufB() { return &P[G::O_BUFB]; }
+  __device__ __forceinline__ float* dfull() { return &P[G::O_DFULL]; }  // d = J' n+ (logical index)
+  __device__ __forceinline__ float* xs() { return &P[G::O_XS]; }        // x by reduced variable
+  __device__ __forceinline__ float* cs() { return &P[G::O_CS]; }        // Givens (c, s), half 1 at +4 words
 };
 static_assert(W_OFF_REC + CMPC_REC_WORDS(MAXN) <= WGeo<80>::PSZ, "prep scratch must fit in P");
 
@@ -136,6 +157,12 @@ __device__ __forceinline__ void wpin(float (&x)[M]) {
   for (int c = 0; c < M; c++) asm volatile("" : "+v"(x[c]));
 }
 
+// rank-2 sweeps (two loads per chunk): a fence every 8 columns keeps the in-flight loads at 16
+// VGPRs (at 16 columns the 128-column class spilled 129 VGPRs)
+#define CMPC_WSWEEP2_FENCE(c)                               \
+  do {                                                      \
+    if (((c) & 7) == 4) __builtin_amdgcn_sched_barrier(0);  \
+  } while (0)
 #define CMPC_WSWEEP_FENCE(c)                                 \
   do {                                                       \
     if (((c) & 15) == 12) __builtin_amdgcn_sched_barrier(0); \
@@ -237,7 +264,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   }
   Model md;
   make_model(srec, P.dt, md);
-  make_bdt<G::NT>(srec, md, t, sh.BdtT);
+  make_bdt<G::NT>(srec, md, t, sh.BdtT());
   wbar();
   if (t < N) {
     float e[13];
@@ -278,7 +305,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     const int cv = real ? sh.varcol[r] : 0;
     float b[13], u1[13], u2[13];
 #pragma unroll
-    for (int j = 0; j < 13; j++) b[j] = real ? sh.BdtT[cv][j] : 0.f;
+    for (int j = 0; j < 13; j++) b[j] = real ? sh.BdtT()[cv][j] : 0.f;
     n1_mul(md, b, u1);
     n1_mul(md, u1, u2);
     {
@@ -303,12 +330,14 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       recur(md, wts, gk, z);
       const int wb = __builtin_amdgcn_readfirstlane(sh.blkbase[i]);
       const int we = __builtin_amdgcn_readfirstlane(sh.blkbase[i + 1]);
+      // half h takes every other column of the step (the per-foot unrolled form of class 1, with
+      // both halves computing every column, measured 2-5 % slower at N = 16 / 20)
       for (int w0 = wb; w0 < we; w0 += 2) {
         const int w = w0 + h;
         const int cw = sh.varcol[w];
         float bw[13];
 #pragma unroll
-        for (int j = 0; j < 13; j++) bw[j] = sh.BdtT[cw][j];
+        for (int j = 0; j < 13; j++) bw[j] = sh.BdtT()[cw][j];
         float val = 2.f * dot13(bw, z);
         if (w == r) val += P.alpha2;  // qH = 2 (B'SB + alpha I), SolverMPC.cpp:806
         if (act && w < we && w >= r) sh.P[myrow + w] = val;
@@ -337,6 +366,62 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   // published into P's row k (even / odd segments), one s_barrier per step
   int status = CMPC_OK;
   float my_inv = 1.f;
+#if CMPC_WIDE_CHOL2
+  // Two pivots per step (k even, k+1: register k/2 of half 0 and of half 1 of every row), one
+  // s_barrier per step instead of per pivot. Each lane publishes its own pivot column entry
+  // (half 0: raw column k, half 1: raw column k+1), then every row applies both steps as one
+  // rank-2 sweep over the two raw columns:
+  //   beta = H[k+1][k] / d_k, d_k+1 = H[k+1][k+1] - beta H[k+1][k], s1 = H[r][k+1] - beta H[r][k],
+  //   a1 = -s1 / d_k+1, a0 = -H[r][k] / d_k - beta a1   (coefficient of the raw column k)
+  // J = L^-T below applies the same beta to the stored raw column k+1. Odd n: the last step's
+  // second pivot is the identity padding row.
+  static_for<0, NV / 2>([&](auto KB) {
+    constexpr int k = 2 * decltype(KB)::value, k1 = k + 1;
+    constexpr int kj = k >> 1;
+    constexpr int j0 = G::j0(k);  // = j0(k + 1)
+    constexpr int base = G::fbase(k), base1 = G::fbase(k1);
+    constexpr int st = G::seg(k);  // = seg(k + 1)
+    if (k < n) {
+      const float mine = slot[kj];
+      const float other = pair_other(mine, h);
+      const float hk = h ? other : mine;    // H[r][k]
+      const float hk1 = h ? mine : other;   // H[r][k+1]
+      // two stores with constant bases (one store with a per-lane base select made the 128-column
+      // class spill 129 VGPRs)
+      if (h == 0 && r >= 2 * j0 && r < NV) sh.P[base + (r & 1) * st + (r >> 1) - j0] = (r >= k) ? mine : 0.f;
+      if (h == 1 && r >= 2 * j0 && r < NV) sh.P[base1 + (r & 1) * st + (r >> 1) - j0] = (r >= k1) ? mine : 0.f;
+      if (h == 0 && (r == k || r == k1)) sh.gbuf()[r] = gb;
+      wbar();
+      float d0 = sh.P[base + kj - j0];
+      const float h10 = sh.P[base + st + kj - j0];
+      const float d1r = sh.P[base1 + st + kj - j0];
+      const float g0 = sh.gbuf()[k], g1 = sh.gbuf()[k1];
+      if (!(d0 > 0.f)) { status = CMPC_NOT_PD; d0 = 1e-30f; }
+      const float i0 = __builtin_amdgcn_rsqf(d0);  // raw v_rsq: d is a normal positive pivot
+      const float beta = h10 * (i0 * i0);
+      float d1 = fmaf(-h10, beta, d1r);
+      if (!(d1 > 0.f)) { status = CMPC_NOT_PD; d1 = 1e-30f; }
+      const float i1 = __builtin_amdgcn_rsqf(d1);
+      if (r == k) { my_inv = i0; if (h == 0) sh.ibuf()[k] = i0; }
+      if (r == k1) { my_inv = i1; if (h == 0) sh.ibuf()[k1] = i1; }
+      const float s1 = fmaf(-hk, beta, hk1);
+      const float a1 = (r > k1 && r < NV) ? -s1 * (i1 * i1) : 0.f;
+      const float a0 = (r > k && r < NV) ? fmaf(-a1, beta, -hk * (i0 * i0)) : 0.f;
+      const float* prow0 = &sh.P[base + h * st - j0];
+      const float* prow1 = &sh.P[base1 + h * st - j0];
+#pragma unroll
+      for (int j = j0; j < NH; j += 4) {
+        const float4 r0 = *reinterpret_cast<const float4*>(prow0 + j);
+        const float4 r1 = *reinterpret_cast<const float4*>(prow1 + j);
+        axpy4(a0, r0, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+        axpy4(a1, r1, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+        CMPC_WSWEEP2_FENCE(j);
+      }
+      gb = fmaf(a1, g1, fmaf(a0, g0, gb));
+      wpin(slot);
+    }
+  });
+#else
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int kj = k >> 1, kh = k & 1;
@@ -349,12 +434,12 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       const float hrk = (h == kh) ? mine : other;          // H[r][k] of the trailing matrix
       if (h == kh && r >= 2 * j0 && r < NV)
         sh.P[base + (r & 1) * st + (r >> 1) - j0] = (r >= k) ? mine : 0.f;
-      if (r == k && h == 0) sh.gbuf[k] = gb;
+      if (r == k && h == 0) sh.gbuf()[k] = gb;
       wbar();
       float d = sh.P[base + kh * st + kj - j0];
       if (!(d > 0.f)) { status = CMPC_NOT_PD; d = 1e-30f; }
       const float inv = __builtin_amdgcn_rsqf(d);  // raw v_rsq: d is a normal positive pivot
-      if (r == k) { my_inv = inv; if (h == 0) sh.ibuf[k] = inv; }
+      if (r == k) { my_inv = inv; if (h == 0) sh.ibuf()[k] = inv; }
       const float a = (r > k && r < NV) ? -hrk * (inv * inv) : 0.f;
       const float* prow = &sh.P[base + h * st - j0];
 #pragma unroll
@@ -363,12 +448,13 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         axpy4(a, r4, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
         CMPC_WSWEEP_FENCE(j);
       }
-      gb = fmaf(a, sh.gbuf[k], gb);
+      gb = fmaf(a, sh.gbuf()[k], gb);
       wpin(slot);
     }
   });
+#endif
   const float yv = real ? gb * my_inv : 0.f;  // L y = g
-  if (h == 0 && r < NV) sh.ybuf[r & 1][r >> 1] = yv;
+  if (h == 0 && r < NV) sh.ybuf(r & 1)[r >> 1] = yv;
   wbar();
 
 #if CMPC_DIAG_STOP != 1  // diagnostic builds: stop after the Cholesky (1) / after J (2)
@@ -385,6 +471,40 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       slot[j] = (lr == -2 * j) ? 1.f : 0.f;
     });
   }
+#if CMPC_WIDE_J2
+  // two columns per step, as the factorisation (the stored column k+1 is raw: beta corrects it)
+  static_for<0, NV / 2>([&](auto KB) {
+    constexpr int k = 2 * decltype(KB)::value, k1 = k + 1;
+    constexpr int kj = k >> 1;
+    constexpr int j0 = G::j0(k);
+    constexpr int base = G::fbase(k), base1 = G::fbase(k1);
+    constexpr int st = G::seg(k);
+    if (k < n) {
+      wlsync();
+      const float i0 = sh.ibuf()[k], i1 = sh.ibuf()[k1];
+      const float h10 = sh.P[base + st + kj - j0];
+      const float beta = h10 * (i0 * i0);
+      const float mine = slot[kj];
+      const float other = pair_other(mine, h);
+      const float x0 = (h ? other : mine) * i0;
+      const float x1 = fmaf(-h10 * i0, x0, h ? mine : other) * i1;
+      const float a1 = -x1 * i1;
+      const float a0 = fmaf(-a1, beta, -x0 * i0);
+      const float* prow0 = &sh.P[base + h * st - j0];
+      const float* prow1 = &sh.P[base1 + h * st - j0];
+#pragma unroll
+      for (int j = j0; j < NH; j += 4) {
+        const float4 r0 = *reinterpret_cast<const float4*>(prow0 + j);
+        const float4 r1 = *reinterpret_cast<const float4*>(prow1 + j);
+        axpy4(a0, r0, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+        axpy4(a1, r1, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+        CMPC_WSWEEP2_FENCE(j);
+      }
+      slot[kj] = h ? x1 : x0;
+      wpin(slot);
+    }
+  });
+#else
   static_for<0, NV>([&](auto KC) {
     constexpr int k = decltype(KC)::value;
     constexpr int kj = k >> 1, kh = k & 1;
@@ -393,7 +513,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     constexpr int st = G::seg(k);
     if (k < n) {
       wlsync();
-      const float inv = sh.ibuf[k];
+      const float inv = sh.ibuf()[k];
       const float mine = slot[kj];
       const float other = pair_other(mine, h);
       const float xk = ((h == kh) ? mine : other) * inv;
@@ -411,11 +531,12 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   });
 
 #endif
+#endif
   // ---- unconstrained minimiser x = -J y
   float xv;
   {
     f2v xacc = {0.f, 0.f};
-    const float* yb = &sh.ybuf[h][0];
+    const float* yb = sh.ybuf(h);
 #pragma unroll
     for (int j = 0; j < NH; j += 4) {
       const float4 y4 = *reinterpret_cast<const float4*>(yb + j);
@@ -448,7 +569,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       const int h = lane >> 5;
       const int r = 32 * wave + (lane & 31);
       if (p < 0) {
-        if (h == 0 && r < NV) sh.xs[r] = xv;
+        if (h == 0 && r < NV) sh.xs()[r] = xv;
         wbar();
         // most violated constraint (normalised slack); every wave scans the same foot-steps
         float best = 0.f, xm = 0.f;
@@ -457,7 +578,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         for (int m = 0; m < 2; m++) {
           const int s = lane + 64 * m;
           if (s < nfs) {
-            const float fx = sh.xs[3 * s], fy = sh.xs[3 * s + 1], fz = sh.xs[3 * s + 2];
+            const float fx = sh.xs()[3 * s], fy = sh.xs()[3 * s + 1], fz = sh.xs()[3 * s + 2];
             xm = fmaxf(xm, fmaxf(fabsf(fx), fmaxf(fabsf(fy), fabsf(fz))));
             float sl[6];
             sl[0] = (mui * fx + fz) * fnorm;
@@ -483,34 +604,34 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       // d = J' n+ : rows ia, iz of J through LDS (logical order)
       if (r == cp.ia && cp.ia != cp.iz) {
 #pragma unroll
-        for (int j = 0; j < NH; j++) sh.bufA[h * G::HOFF + j] = slot[j];
+        for (int j = 0; j < NH; j++) sh.bufA()[h * G::HOFF + j] = slot[j];
       }
       if (r == cp.iz) {
 #pragma unroll
-        for (int j = 0; j < NH; j++) sh.bufB[h * G::HOFF + j] = slot[j];
+        for (int j = 0; j < NH; j++) sh.bufB()[h * G::HOFF + j] = slot[j];
       }
-      if (h == 0 && r < NV) sh.xs[r] = xv;
+      if (h == 0 && r < NV) sh.xs()[r] = xv;
       wbar();
       // thread t < NV: logical column t
       float dv = 0.f, dm = 0.f;
       if (t < NV) {
         const int li = lidx<NV>(t);
-        dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA[li], cp.cb * sh.bufB[li]) : cp.cb * sh.bufB[li];
+        dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.bufA()[li], cp.cb * sh.bufB()[li]) : cp.cb * sh.bufB()[li];
         dm = (t >= q) ? dv : 0.f;
-        sh.vbuf[li] = dm;
-        sh.dfull[t] = dv;
+        sh.vbuf()[li] = dm;
+        sh.dfull()[t] = dv;
       }
       {
         const float dw = wave_sum(dv * dv);
         if (lane == 0) sh.redf[wave] = dw;
       }
-      const float spv = fmaf(cp.ca, sh.xs[cp.ia], fmaf(cp.cb, sh.xs[cp.iz], -cp.bp));
+      const float spv = fmaf(cp.ca, sh.xs()[cp.ia], fmaf(cp.cb, sh.xs()[cp.iz], -cp.bp));
       wbar();
       // z_r = J_r . dm (primal step direction), zn = |dm|^2 = z' n+, dn = |d|^2
       float zv, zn, dn = 0.f;
       {
         f2v zacc = {0.f, 0.f}, nacc = {0.f, 0.f};
-        const float* vb = &sh.vbuf[h * G::HOFF];
+        const float* vb = &sh.vbuf()[h * G::HOFF];
 #pragma unroll
         for (int j = 0; j < NH; j += 4) {
           const float4 m4 = *reinterpret_cast<const float4*>(vb + j);
@@ -531,7 +652,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         float acc[RQ];
 #pragma unroll
         for (int m = 0; m < RQ; m++) {
-          acc[m] = (lane + 64 * m < NV) ? sh.dfull[(lane + 64 * m) < NV ? lane + 64 * m : 0] : 0.f;
+          acc[m] = (lane + 64 * m < NV) ? sh.dfull()[(lane + 64 * m) < NV ? lane + 64 * m : 0] : 0.f;
           r_a[m] = 0.f;
         }
         for (int i = q - 1; i >= 0; i--) {
@@ -577,12 +698,12 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       if (add) {
         // ---- add p: Householder reflection on logical columns q.., R gains column (d1, -sgn ts)
         const float ts = sqrtf(zn);
-        const float dq = sh.dfull[q];
+        const float dq = sh.dfull()[q];
         const float sgn = (dq >= 0.f) ? 1.f : -1.f;
         beta = fast_rcp(ts * (ts + fabsf(dq)));  // 2 / (w'w)
         if (t < NV) {
-          sh.vbuf[lidx<NV>(t)] = (t == q) ? dq + sgn * ts : dm;
-          *reinterpret_cast<float2*>(&sh.cs[2 * t + (t >= NH ? 4 : 0)]) = make_float2(1.f, 0.f);
+          sh.vbuf()[lidx<NV>(t)] = (t == q) ? dq + sgn * ts : dm;
+          *reinterpret_cast<float2*>(&sh.cs()[2 * t + (t >= NH ? 4 : 0)]) = make_float2(1.f, 0.f);
           const int offq = rcol_w(q);
           if (t < q) sh.P[offq + t] = dv;
           if (t == q) sh.P[offq + q] = -sgn * ts;
@@ -599,9 +720,9 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         const int k = kk;
         seam = (q > NH);
         if (t < NV) {
-          sh.vbuf[lidx<NV>(t)] = 0.f;
+          sh.vbuf()[lidx<NV>(t)] = 0.f;
           if (t < k || t > q - 2)
-            *reinterpret_cast<float2*>(&sh.cs[2 * t + (t >= NH ? 4 : 0)]) = make_float2(1.f, 0.f);
+            *reinterpret_cast<float2*>(&sh.cs()[2 * t + (t >= NH ? 4 : 0)]) = make_float2(1.f, 0.f);
         }
         if (wave == 0) {
           const int ak = rli_pos<RQ>(a_a, k);
@@ -671,7 +792,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
               }
             }
             if (lane == 0)
-              *reinterpret_cast<float2*>(&sh.cs[2 * j + (j >= NH ? 4 : 0)]) = make_float2(cc, sn);
+              *reinterpret_cast<float2*>(&sh.cs()[2 * j + (j >= NH ? 4 : 0)]) = make_float2(cc, sn);
             wlsync();
           }
         }
@@ -680,7 +801,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       // J <- J (I - beta w w'): tw = J_r . w over both halves, J_r -= beta tw w (no-op on a drop)
       {
         f2v tacc = {0.f, 0.f};
-        const float* vb = &sh.vbuf[h * G::HOFF];
+        const float* vb = &sh.vbuf()[h * G::HOFF];
 #pragma unroll
         for (int j = 0; j < NH; j += 4) {
           const float4 w4 = *reinterpret_cast<const float4*>(vb + j);
@@ -697,7 +818,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         }
       }
       // J columns (l, l+1) <- Givens chain, ascending l (identity on an add)
-      const float* csb = &sh.cs[h * (2 * NH + 4)];
+      const float* csb = &sh.cs()[h * (2 * NH + 4)];
       if (!seam) {
         // every rotation lies in half 0 (active set <= NV/2); half 1 reads identities
         static_for<0, NH - 1>([&](auto JC) {
@@ -720,7 +841,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
           if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
         });
         {
-          const float2 c2 = *reinterpret_cast<const float2*>(&sh.cs[2 * (NH - 1)]);
+          const float2 c2 = *reinterpret_cast<const float2*>(&sh.cs()[2 * (NH - 1)]);
           const float mine = h ? slot[0] : slot[NH - 1];
           const float other = pair_other(mine, h);
           if (h == 0) slot[NH - 1] = fmaf(c2.x, mine, c2.y * other);
@@ -762,10 +883,19 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
 
 }  // namespace
 
-// One workgroup per possible entry of the class's list (the list length is only known on the
-// device); surplus workgroups exit after one load. (Persistent workgroups that dequeue list
-// entries were measured to spill — w128: 168 VGPRs + 48 spilled, 256 SGPR spills — and were
-// dropped.)
+// CMPC_WIDE_PERSIST (per width unit; on for the 144-, 192- and 256-column classes, whose
+// workgroups are the largest and the most often empty): persistent workgroups over the class's
+// list: as many as fit the GPU at this kernel's occupancy
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs, at most one per list slot), each dequeues
+// list entries with one global atomic until the list is exhausted. The list length is only known
+// on the device; a grid of one workgroup per possible entry made the GPU drain up to `batch` empty
+// workgroups per class (3.5 ms for the 146-KB workgroups of the 256 class at config 5, 1.2 ms for
+// the 192 class). With deq == nullptr (single-instance path) workgroup i takes entry i. The
+// persistent loop costs the 128 class 4 spilled VGPRs, so the populous classes keep one workgroup
+// per possible list entry.
+#ifndef CMPC_WIDE_PERSIST
+#define CMPC_WIDE_PERSIST 0
+#endif
 #if CMPC_WIDE_VGPR_CAP > 0
 #define CMPC_WIDE_VGPR_ATTR __attribute__((amdgpu_num_vgpr(CMPC_WIDE_VGPR_CAP)))
 #else
@@ -778,6 +908,7 @@ struct WideArgs {
   int32_t* iters;
   const int* in_list;
   const int* in_count;
+  int* deq;
   KParams P;
 };
 
@@ -785,19 +916,52 @@ template <int NV>
 __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGPR_ATTR void cmpc_solve_w_kernel(
     WideArgs A) {
   __shared__ SharedW<NV> sh;
-  const int b = blockIdx.x;
-  if (b >= *A.in_count) return;
-  const int inst = A.in_list[b];
-  solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
-              A.status + inst, A.iters ? A.iters + inst : nullptr);
+  const int count = *A.in_count;
+#if !CMPC_WIDE_PERSIST
+  {  // one workgroup per possible list entry
+    const int b = blockIdx.x;
+    if (b >= count) return;
+    const int inst = A.in_list[b];
+    solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
+                A.status + inst, A.iters ? A.iters + inst : nullptr);
+  }
+#else
+  for (int round = 0;; round++) {
+    // deq == nullptr (single-instance path): workgroup i takes entry i, once
+    if (threadIdx.x == 0) sh.deq_b = A.deq ? atomicAdd(A.deq, 1) : (round == 0 ? (int)blockIdx.x : count);
+    wbar();
+    const int b = __builtin_amdgcn_readfirstlane(sh.deq_b);
+    if (b >= count) break;
+    const int inst = A.in_list[b];
+    solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
+                A.status + inst, A.iters ? A.iters + inst : nullptr);
+    wbar();  // every wave is done with this instance's LDS before the next record lands there
+  }
+#endif
+}
+
+template <int NV>
+int wide_grid_cap() {
+  static const int cap = [] {
+    int nb = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc_solve_w_kernel<NV>, WGeo<NV>::NT, 0) !=
+            hipSuccess || nb <= 0)
+      nb = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    return nb * cus;
+  }();
+  return cap;
 }
 
 template <int NV>
 hipError_t launch_wide_impl(const float* d_recs, const KParams& P, float* d_forces,
                             uint8_t* d_status, int32_t* d_iters, const int* in_list,
-                            const int* in_count, int grid, hipStream_t stream) {
+                            const int* in_count, int* deq, int grid, hipStream_t stream) {
   if (grid <= 0) return hipSuccess;
-  const WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, in_count, P};
+  if (CMPC_WIDE_PERSIST && deq) grid = grid < wide_grid_cap<NV>() ? grid : wide_grid_cap<NV>();
+  const WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, in_count, deq, P};
   hipLaunchKernelGGL(cmpc_solve_w_kernel<NV>, dim3(grid), dim3(WGeo<NV>::NT), 0, stream, A);
   return hipGetLastError();
 }

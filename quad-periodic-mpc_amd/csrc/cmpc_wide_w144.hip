@@ -4,14 +4,15 @@
 #ifndef CMPC_WIDE_WAVES_PER_EU
 #define CMPC_WIDE_WAVES_PER_EU 3
 #endif
+#define CMPC_WIDE_PERSIST 1  // persistent workgroups dequeue the list (cmpc_wide.h)
 #include "cmpc_wide.h"
 
 namespace cmpc {
 
 hipError_t launch_wide_w144(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
-                          int32_t* d_iters, const int* in_list, const int* in_count, int grid,
+                          int32_t* d_iters, const int* in_list, const int* in_count, int* deq, int grid,
                           hipStream_t stream) {
-  return launch_wide_impl<144>(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, grid,
+  return launch_wide_impl<144>(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid,
                               stream);
 }
 

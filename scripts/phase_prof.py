@@ -21,6 +21,9 @@ sys.path.insert(0, ROOT)
 PROF_LIB = os.path.join(ROOT, "quad-periodic-mpc_amd", "libcmpc_prof.so")
 STAGES = ["prep (stance, model, gradient recursion)", "condensation H", "Cholesky [H|g]",
           "J = L^-T", "active set (x = -Jy, GI loop)", "scatter"]
+GI_SEGS = ["select the most violated constraint", "export J rows, d, z = J d, |d|^2",
+           "back substitution, step lengths", "add / drop: R update", "J reflection (every trip)",
+           "J Givens chain (drops)"]
 
 
 def main():
@@ -47,7 +50,7 @@ def main():
     status = torch.empty(B, dtype=torch.uint8, device="cuda")
     iters = torch.empty(B, dtype=torch.int32, device="cuda")
     s = solver_mod.BatchSolver(cm.make_params(N), max_batch=B)
-    out = (ctypes.c_ulonglong * 8)()
+    out = (ctypes.c_ulonglong * 16)()
     s.solve(recs, forces, status, iters)
     torch.cuda.synchronize()
     lib.cmpc_debug_phase_read(out)  # reset after the warm-up solve
@@ -63,6 +66,10 @@ def main():
           f"{v[7] / inst:.2f}, mean {tot / inst:.0f} cycles / instance")
     for i, name in enumerate(STAGES):
         print(f"  {name:45s} {v[i] / inst:10.0f} cyc  {100 * v[i] / tot:5.1f} %")
+    trips = max(v[7], 1.0)
+    print(f"  active-set trips {int(v[7])}, drops {int(v[14])}; per trip:")
+    for i, name in enumerate(GI_SEGS):
+        print(f"    {name:43s} {v[8 + i] / trips:10.0f} cyc")
     s.close()
 
 
