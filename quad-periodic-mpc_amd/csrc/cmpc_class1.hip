@@ -34,6 +34,10 @@
 #ifndef CMPC_C1_RL
 #define CMPC_C1_RL 0
 #endif
+// chunks per group of the software-pipelined vector sweeps (piped_sweep)
+#ifndef C1_PIPE_GRP
+#define C1_PIPE_GRP 4
+#endif
 // Cholesky two pivots per step (rank-2 sweeps); 0: one pivot per step
 #ifndef CMPC_C1_CHOL2
 #define CMPC_C1_CHOL2 1
@@ -511,12 +515,12 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   sh.vbuf[v] = yv;
   lsync();
   f2v xacc = {0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < NV; c += 4) {
-    const float4 y4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-    dot4(xacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], y4);
-    CMPC_SWEEP_FENCE(c);
-  }
+  piped_sweep<0, NV, C1_PIPE_GRP>(
+      [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf[decltype(C)::value]); },
+      [&](auto C, float4 y4) {
+        constexpr int c = decltype(C)::value;
+        dot4(xacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], y4);
+      });
   float xv = (v < n) ? -(xacc.x + xacc.y) : 0.f;
   lsync();
 
@@ -589,13 +593,13 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       lsync();
       // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+, dn = |d|^2
       f2v zacc = {0.f, 0.f}, nacc = {0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < NV; c += 4) {
-        const float4 m4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-        dot4(zacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], m4);
-        dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
-        CMPC_SWEEP_FENCE(c);
-      }
+      piped_sweep<0, NV, C1_PIPE_GRP>(
+          [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf[decltype(C)::value]); },
+          [&](auto C, float4 m4) {
+            constexpr int c = decltype(C)::value;
+            dot4(zacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], m4);
+            dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
+          });
       float zv = zacc.x + zacc.y, zn = nacc.x + nacc.y;
       // materialise both sums here: otherwise the FMAs sink below the back substitution loop
       // and the NV loaded values of vbuf stay live across it (158 VGPRs, three waves per SIMD)
@@ -702,22 +706,22 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       {
         // J <- J (I - beta w w'): tw = J_v . w, J_v -= beta tw w  (no-op on a drop: beta = 0)
         f2v tacc = {0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < NV; c += 4) {
-          const float4 w4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-          dot4(tacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], w4);
-          CMPC_SWEEP_FENCE(c);
-        }
+        piped_sweep<0, NV, C1_PIPE_GRP>(
+            [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf[decltype(C)::value]); },
+            [&](auto C, float4 w4) {
+              constexpr int c = decltype(C)::value;
+              dot4(tacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], w4);
+            });
         const float bt = -beta * (tacc.x + tacc.y);
         // re-read w from LDS: without this point the compiler keeps all NV values of the first
         // sweep's loads live for the second (a whole row of extra VGPRs)
         asm volatile("" ::: "memory");
-#pragma unroll
-        for (int c = 0; c < NV; c += 4) {
-          const float4 w4 = *reinterpret_cast<const float4*>(&sh.vbuf[c]);
-          axpy4(bt, w4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
-          CMPC_SWEEP_FENCE(c);
-        }
+        piped_sweep<0, NV, C1_PIPE_GRP>(
+            [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf[decltype(C)::value]); },
+            [&](auto C, float4 w4) {
+              constexpr int c = decltype(C)::value;
+              axpy4(bt, w4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);
+            });
       }
       C1_SUB(4);
       if (!add_u) {

@@ -118,6 +118,14 @@ __device__ __forceinline__ int tid_opq() {
   return x;
 }
 
+// lane id (0..63) from mbcnt, opaque to the optimiser: unlike threadIdx.x (v0 at entry, which
+// has to stay live, or be spilled, to be re-read later) it needs no register between uses
+__device__ __forceinline__ int lane_opq() {
+  int x = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 template <int I, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < E) {
@@ -125,6 +133,41 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for<I + 1, E>(f);
   }
 }
+// Software-pipelined sweep over 16-B chunks c = C0, C0 + 4, ..., < CE: ld(c) loads chunk c's
+// operands from LDS, f(c, v) consumes them; in groups of GRP chunks, the loads of group g + 1 are
+// issued before the arithmetic of group g (scheduling fences keep that order and bound the live
+// loads to two groups), so the wave meets the LDS latency once per sweep, not once per group.
+template <int C0, int CE, int GRP, class Ld, class F>
+__device__ __forceinline__ void piped_sweep(Ld&& ld, F&& f) {
+  constexpr int NCH = (CE > C0) ? (CE - C0) / 4 : 0;
+  if constexpr (NCH > 0) {
+    using T = decltype(ld(std::integral_constant<int, C0>{}));
+    constexpr int NG = (NCH + GRP - 1) / GRP;
+    T cur[GRP], nxt[GRP];
+    static_for<0, GRP>([&](auto I) {
+      constexpr int ch = decltype(I)::value;
+      if constexpr (ch < NCH) cur[ch] = ld(std::integral_constant<int, C0 + 4 * ch>{});
+    });
+    static_for<0, NG>([&](auto GI) {
+      constexpr int g = decltype(GI)::value;
+      static_for<0, GRP>([&](auto I) {
+        constexpr int ch = (g + 1) * GRP + decltype(I)::value;
+        if constexpr (ch < NCH) nxt[decltype(I)::value] = ld(std::integral_constant<int, C0 + 4 * ch>{});
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, GRP>([&](auto I) {
+        constexpr int ch = g * GRP + decltype(I)::value;
+        if constexpr (ch < NCH) f(std::integral_constant<int, C0 + 4 * ch>{}, cur[decltype(I)::value]);
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, GRP>([&](auto I) { cur[decltype(I)::value] = nxt[decltype(I)::value]; });
+    });
+  }
+}
+struct F4x2 {
+  float4 a, b;
+};
+
 // An SGPR value the compiler cannot see through: keeps per-iteration scalar work of an unrolled
 // loop inside its iteration (otherwise LICM hoists dozens of SGPRs out of it -> spills).
 __device__ __forceinline__ int opaque(int x) {

@@ -195,6 +195,19 @@ __device__ __forceinline__ int rli_pos(const int (&a)[RQ], int i) {
   return x;
 }
 
+// the lane's thread id, row and half, re-derived where needed (lane_opq): the ids of the top of
+// solve_w would otherwise stay live across the unrolled factorisation (at five waves per SIMD
+// they were spilled and reloaded from scratch once per pivot step)
+#define CMPC_WIDE_IDS()                              \
+  const int t = 64 * wave + lane_opq();              \
+  const int lane = t & 63;                           \
+  const int h = lane >> 5;                           \
+  const int r = 32 * wave + (lane & 31);             \
+  (void)t;                                           \
+  (void)lane;                                        \
+  (void)h;                                           \
+  (void)r
+
 template <int NV>
 __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KParams& P,
                                         SharedW<NV>& sh, float* __restrict__ fout,
@@ -382,6 +395,10 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     constexpr int base = G::fbase(k), base1 = G::fbase(k1);
     constexpr int st = G::seg(k);  // = seg(k + 1)
     if (k < n) {
+      // row / half re-derived from an opaque thread index each step: a row index kept live
+      // across the unrolled steps was spilled at five waves per SIMD (wide 96) and reloaded from
+      // scratch twice per step
+      CMPC_WIDE_IDS();
       const float mine = slot[kj];
       const float other = pair_other(mine, h);
       const float hk = h ? other : mine;    // H[r][k]
@@ -453,8 +470,12 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     }
   });
 #endif
-  const float yv = real ? gb * my_inv : 0.f;  // L y = g
-  if (h == 0 && r < NV) sh.ybuf(r & 1)[r >> 1] = yv;
+  float yv;
+  {
+    CMPC_WIDE_IDS();
+    yv = (r < n) ? gb * my_inv : 0.f;  // L y = g
+    if (h == 0 && r < NV) sh.ybuf(r & 1)[r >> 1] = yv;
+  }
   wbar();
 
 #if CMPC_DIAG_STOP != 1  // diagnostic builds: stop after the Cholesky (1) / after J (2)
@@ -464,7 +485,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     // the unit row from an opaque thread index: with the plain (h, r) the NH per-lane column
     // ids 2 j + h are shared (CSE) with the H-row load above and stay live across the whole
     // Cholesky (64 VGPRs at NV = 128)
-    const int to = tid_opq();
+    const int to = 64 * wave + lane_opq();
     const int lr = ((to & 63) >> 5) - 32 * (to >> 6) - (to & 31);  // h - r
     static_for<0, NH>([&](auto J) {
       constexpr int j = decltype(J)::value;
@@ -481,6 +502,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     constexpr int st = G::seg(k);
     if (k < n) {
       wlsync();
+      const int h = (lane_opq() >> 5) & 1;
       const float i0 = sh.ibuf()[k], i1 = sh.ibuf()[k1];
       const float h10 = sh.P[base + st + kj - j0];
       const float beta = h10 * (i0 * i0);
@@ -535,6 +557,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   // ---- unconstrained minimiser x = -J y
   float xv;
   {
+    CMPC_WIDE_IDS();
     f2v xacc = {0.f, 0.f};
     const float* yb = sh.ybuf(h);
 #pragma unroll
@@ -544,7 +567,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       CMPC_WSWEEP_FENCE(j);
     }
     const float xs2 = pair_sum(xacc.x + xacc.y);
-    xv = real ? -xs2 : 0.f;
+    xv = (r < n) ? -xs2 : 0.f;
   }
   wbar();  // the factor rows in P are dead from here; P holds R
 
@@ -564,10 +587,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   if (status == CMPC_OK && CMPC_DIAG_STOP == 0) {
     for (;;) {
       wpin(slot);
-      const int t = tid_opq();
-      const int lane = t & 63;
-      const int h = lane >> 5;
-      const int r = 32 * wave + (lane & 31);
+      CMPC_WIDE_IDS();
       if (p < 0) {
         if (h == 0 && r < NV) sh.xs()[r] = xv;
         wbar();
@@ -693,6 +713,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       up += tt;
       if (!zero_step) xv = fmaf(tt, zv, xv);
       const bool add = !zero_step && t2 <= t1;
+      const bool add_u = __builtin_amdgcn_readfirstlane((int)add) != 0;  // wave-uniform copy
       float beta = 0.f;
       bool seam = false;   // a drop whose Givens chain crosses into half 1
       if (add) {
@@ -818,8 +839,10 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         }
       }
       // J columns (l, l+1) <- Givens chain, ascending l (identity on an add)
+      // (drops only: on an add every rotation is the identity)
       const float* csb = &sh.cs()[h * (2 * NH + 4)];
-      if (!seam) {
+      if (add_u) {
+      } else if (!seam) {
         // every rotation lies in half 0 (active set <= NV/2); half 1 reads identities
         static_for<0, NH - 1>([&](auto JC) {
           constexpr int j = decltype(JC)::value;
@@ -868,16 +891,19 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
 
   // ---- scatter (q_soln layout 12 k + 3 leg + axis, swing -> 0) staged in LDS, coalesced out
   const bool ok = (status == CMPC_OK);
-  wbar();
-  for (int i = t; i < 12 * N; i += G::NT) sh.P[i] = 0.f;
-  wbar();
-  if (ok && h == 0 && real) sh.P[12 * sh.varblk[r] + sh.varcol[r]] = xv;
-  wbar();
-  for (int i = 4 * t; i < 12 * N; i += 4 * G::NT)
-    *reinterpret_cast<float4*>(&fout[i]) = *reinterpret_cast<const float4*>(&sh.P[i]);
-  if (t == 0) {
-    st_out[0] = (uint8_t)status;
-    if (it_out) it_out[0] = iters;
+  {
+    CMPC_WIDE_IDS();
+    wbar();
+    for (int i = t; i < 12 * N; i += G::NT) sh.P[i] = 0.f;
+    wbar();
+    if (ok && h == 0 && r < n) sh.P[12 * sh.varblk[r] + sh.varcol[r]] = xv;
+    wbar();
+    for (int i = 4 * t; i < 12 * N; i += 4 * G::NT)
+      *reinterpret_cast<float4*>(&fout[i]) = *reinterpret_cast<const float4*>(&sh.P[i]);
+    if (t == 0) {
+      st_out[0] = (uint8_t)status;
+      if (it_out) it_out[0] = iters;
+    }
   }
 }
 

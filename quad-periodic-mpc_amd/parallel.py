@@ -152,15 +152,18 @@ class ShardedSolver:
             self._solver = None
 
 
-# Smallest pipeline piece worth cutting: below ~16384 instances a solve no longer fills the GPU's
-# 4096 class-1 wave slots several times over and the per-instance rate drops.
-MIN_PIECE = 16384
+# Smallest pipeline piece worth cutting. Every solve ends in a tail (its slowest instances, the
+# wide size classes) that a piece pays again; measured on one MI355X (scripts/occupancy_sweep.py):
+# 32768 instances in one solve 1.23 ms, in two pieces of 16384 2 x 0.83 ms; 65536 in one 1.8 ms.
+# The xGMI time a second piece could hide at 8 ranks (~0.25 ms per step) is less than the 0.4 ms
+# it costs, so pieces stay at >= 65536 instances.
+MIN_PIECE = 65536
 MAX_CHUNKS = 4
 
 
 def auto_chunks(local_batch: int, min_piece: int = MIN_PIECE, max_chunks: int = MAX_CHUNKS) -> int:
     """Pieces per rank for the config-4 pipeline: as many as keep every piece >= ``min_piece``
-    instances, at most ``max_chunks`` (262144 over 1 / 2 / 4 / 8 ranks -> 4 / 4 / 4 / 2)."""
+    instances, at most ``max_chunks`` (262144 over 1 / 2 / 4 / 8 ranks -> 4 / 2 / 1 / 1)."""
     return max(1, min(max_chunks, local_batch // max(1, min_piece)))
 
 
