@@ -65,12 +65,18 @@ def algorithmic_bytes(N: int, config5: bool = False) -> int:
     return b + (24 + 1600 + 4 if config5 else 0)
 
 
-def _threads():
+CPU_THREAD_CAP = 16   # the GPU box's CPU share per GPU (its nproc shows the whole machine)
+
+
+def _host_cpus():
     try:
-        n = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+        return os.cpu_count() or 1
+
+
+def _threads():
+    return max(1, min(CPU_THREAD_CAP, _host_cpus()))
 
 
 def cpu_baseline(prm, N: int, config5: bool = False):
@@ -113,6 +119,15 @@ def cpu_baseline(prm, N: int, config5: bool = False):
         orc.ref_solve_batch(lat, prm, nthreads=1)
     lat_us = (time.perf_counter() - t1) / lat.shape[0] * 1e6
     return {"value": round(sample / dt, 1), "unit": "QP solves/s", "cores": threads,
+            "host_cpus_visible": _host_cpus(),
+            "cores_note": (f"capped at {CPU_THREAD_CAP} threads: the GPU box's CPU share per GPU "
+                           "(the visible count is the whole machine's)"),
+            "condensation_note": ("the condensation is the oracle's plain-C restatement of "
+                                  "SolverMPC.cpp's dense-S products (naive i-p-j loops, gcc -O3 "
+                                  "-march=x86-64-v3), not Eigen: slower per instance than the "
+                                  "reference's Eigen build (SURVEY §0.4 probe with an OpenBLAS "
+                                  "GEMM chain: ~175-205 us per instance); the QP stage is the "
+                                  "reference's own qpOASES"),
             "kind": "reference", "latency_us_1core": round(lat_us, 1),
             "sample": f"{sample} instances of the same synthetic workload (N={N}), per instance "
                       f"{what}the solve_mpc equivalent: fp32 dense-S condensation "
@@ -313,7 +328,12 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
     if pmc:
         vp = {k: pmc[k] for k in ("valu_insts_per_wave", "lds_insts_per_wave", "waves",
                                    "lds_bank_conflict_frac", "wait_frac", "issue_stall_frac",
-                                   "active_frac", "vgpr", "scratch", "pmc_tag") if k in pmc}
+                                   "active_frac", "scratch", "pmc_tag") if k in pmc}
+        if "vgpr" in pmc:
+            # rocprofv3's kernel-trace VGPR_Count: on this image it reads half the compiler's
+            # allocation (80 for class 1's 158 -> 160 registers in round 2); relabelled, not
+            # converted
+            vp["vgpr_count_rocprof_field"] = pmc["vgpr"]
         if "valu_insts_per_wave" in pmc and "waves" in pmc and t1 > 0:
             vp["valu_issue_util"] = round(pmc["valu_insts_per_wave"] * pmc["waves"] * 2.0 /
                                           (1024 * 2.4e9 * t1), 4)

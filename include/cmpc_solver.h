@@ -265,9 +265,10 @@ CMPC_EXTERNC int cmpc_batch_assemble(cmpc_batch* h, float* d_loco, const cmpc_lo
 CMPC_EXTERNC int cmpc_batch_rollout(cmpc_batch* h, float* d_loco, const float* d_records,
                                     const float* d_forces, const float* d_xi6,
                                     const uint8_t* d_due, int batch);
-/* Measurement hooks: record HIP events around each size-class launch of the next `steps`
- * solves; read back per-launch ms pairs [class1, class2] and class 1's overflow count (the
- * number of instances handed to the 2-wave class in the last solve). Synchronises. */
+/* Measurement hooks: record HIP events on the handle's stream around the next `steps` solves;
+ * read back per-solve ms pairs [class 1's launch, the time after it until the wide size classes
+ * have joined] and the number of instances the last solve listed for the wide classes
+ * (n > 64). Synchronises. */
 CMPC_EXTERNC int cmpc_batch_enable_timing(cmpc_batch* h, int steps);
 CMPC_EXTERNC int cmpc_batch_read_timing(cmpc_batch* h, float* ms, int* steps_recorded,
                                         int* class1_overflow);

@@ -18,8 +18,9 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcmpc_hip.so")
 OBJ = os.path.join(ROOT, "build", "obj")
 # one translation unit per kernel family so the large unrolled kernels compile in parallel
-SOURCES = ["cmpc_class1.hip", "cmpc_wide_w80.hip", "cmpc_wide_w96.hip", "cmpc_wide_w128.hip", "cmpc_wide_w144.hip", "cmpc_wide_w192.hip",
-           "cmpc_wide_w256.hip", "cmpc_classg.hip", "cmpc_launch.hip", "cmpc_estimator.hip", "cmpc_assemble.hip",
+SOURCES = ["cmpc_wide_w256.hip", "cmpc_wide_w192.hip", "cmpc_class1.hip", "cmpc_wide_w80.hip", "cmpc_wide_w96.hip",
+           "cmpc_wide_w120.hip", "cmpc_wide_w128.hip", "cmpc_wide_w144.hip", "cmpc_wide_w80p.hip",
+           "cmpc_wide_w96p.hip", "cmpc_wide_w120p.hip", "cmpc_wide_w128p.hip", "cmpc_classg.hip", "cmpc_launch.hip", "cmpc_estimator.hip", "cmpc_assemble.hip",
            "cmpc_admm.hip", "cmpc_quadprog.hip", "cmpc_abi.cpp"]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: the SLP pass packs adjacent row updates into v_pk_fma_f32, which ties

@@ -168,6 +168,7 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
     if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("side streams", e); }
   }
   e = hipEventCreateWithFlags(&h->ctx.fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.classified, hipEventDisableTiming);
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("fork event", e); }
   e = hipMalloc(&h->d_work, sizeof(int) * cmpc::work_ints(max_batch));
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("hipMalloc(work)", e); }
@@ -199,6 +200,7 @@ extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
     if (h->ctx.join[j]) (void)hipEventDestroy(h->ctx.join[j]);
   }
   if (h->ctx.fork) (void)hipEventDestroy(h->ctx.fork);
+  if (h->ctx.classified) (void)hipEventDestroy(h->ctx.classified);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }

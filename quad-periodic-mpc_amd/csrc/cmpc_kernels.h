@@ -35,10 +35,12 @@ struct LocoParams {
 // 128, 192, 256 columns, general), [8 ..) the six lists of max_batch entries each
 // instance lists of the classify pass: 80, 96, 128, 192, 256, G, 144, and 7: class-1 instances
 // with 60 < n <= 64 (the 64-wide class-1 build; n <= 60 runs in the 60-wide build over the
-// whole batch). d_work = [kHdr ints: cnt[0] total, cnt[1 + list] list lengths, cnt[9 + list] the
-// persistent wide workgroups' dequeue counters] [kLists lists of max_batch]
-constexpr int kLists = 8;
-constexpr int kHdr = 16;
+// whole batch); 8: the 120-column wide build (97 <= n <= 120; the 128 build keeps 121..128).
+// d_work = [kHdr ints: cnt[0] total, cnt[1 + list] list lengths, cnt[kDeq + list] the persistent
+// wide workgroups' dequeue counters] [kLists lists of max_batch]
+constexpr int kLists = 9;
+constexpr int kHdr = 32;
+constexpr int kDeq = 16;  // cnt[kDeq + list]: dequeue counter of a persistent class's workgroups
 inline size_t work_ints(int max_batch) { return kHdr + kLists * (size_t)max_batch; }
 // Side streams and events of one handle: the wider size classes run concurrently with class 1
 // (they are latency-bound: few instances, long serial solves). Two side streams: with the
@@ -48,6 +50,7 @@ constexpr int kSideStreams = 2;
 struct LaunchCtx {
   hipStream_t side[kSideStreams] = {nullptr, nullptr};
   hipEvent_t fork = nullptr;
+  hipEvent_t classified = nullptr;  // the classify pass (on side 0) is done
   hipEvent_t join[kSideStreams] = {nullptr, nullptr};
 };
 // Workgroups of the general class (persistent over its overflow list) and its global slabs.
@@ -64,14 +67,19 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
 hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
-// wide classes, two lanes per row, NV/32 wavefronts (cmpc_wide_w{80,96,128,144,192,256}.hip)
+// wide classes, two lanes per row, NV/32 wavefronts (cmpc_wide_w{80,96,120,128,144,192,256}.hip)
 #define CMPC_DECL_WIDE(W)                                                                          \
   hipError_t launch_wide_w##W(const float* d_recs, const KParams& P, float* d_forces,             \
                               uint8_t* d_status, int32_t* d_iters, const int* in_list,            \
                               const int* in_count, int* deq, int grid, hipStream_t stream);
 CMPC_DECL_WIDE(80)
 CMPC_DECL_WIDE(96)
+CMPC_DECL_WIDE(120)
 CMPC_DECL_WIDE(128)
+CMPC_DECL_WIDE(80_persist)
+CMPC_DECL_WIDE(96_persist)
+CMPC_DECL_WIDE(120_persist)
+CMPC_DECL_WIDE(128_persist)
 CMPC_DECL_WIDE(144)
 CMPC_DECL_WIDE(192)
 CMPC_DECL_WIDE(256)

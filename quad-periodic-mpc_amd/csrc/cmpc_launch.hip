@@ -7,6 +7,7 @@
 //     streams forked after classify, so they run concurrently with class 1 and with each
 //     other. At N = 10 they are a latency-bound tail (few, long solves); at N = 16..20 the 128-
 //     and 192-column classes carry the batch and run side by side on the two streams.
+#include <math.h>
 #include <stdlib.h>
 
 #include "cmpc_kernels.h"
@@ -37,8 +38,8 @@ __global__ __launch_bounds__(256) void cmpc_classify_kernel(const float* __restr
       }
     }
     const int n = 3 * nfs;
-    cls = (n <= c1_max) ? -1 : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 128) ? 2 : (n <= 144) ? 6
-        : (n <= 192) ? 3 : (n <= 256) ? 4 : 5;
+    cls = (n <= c1_max) ? -1 : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 120) ? 8
+        : (n <= 128) ? 2 : (n <= 144) ? 6 : (n <= 192) ? 3 : (n <= 256) ? 4 : 5;
   }
   const unsigned long long any = __ballot(cls >= 0);
   if (any == 0ull) return;
@@ -53,6 +54,26 @@ __global__ __launch_bounds__(256) void cmpc_classify_kernel(const float* __restr
     base = __shfl(base, leader);
     if (cls == c) lists[(size_t)c * max_batch + base + __popcll(m & ((1ull << lane) - 1ull))] = i;
   }
+}
+
+// Launch form of the wide class holding n in [lo, hi] (cmpc_wide.h): one workgroup per list entry
+// for the populous classes, persistent workgroups for the sparse ones. Populous: the class meets
+// 6N +- 3 sqrt(N), the trot size (two feet in stance at every step) +- one standard deviation of n
+// = 3 Bin(4N, 1/2) under random contact tables. Measured (profiles/r03_ab/r03_e): every class
+// one-per-entry lost config 5 2 % to the drains of the sparse classes; every class persistent
+// lost config 3 / 2 2-6 % to the spills of the 80-column persistent build. Below 16384 instances
+// (the same threshold as class 1's split) the drains are short and every class is one-per-entry
+// (config 2: 11.3 M -> 11.7 M QP/s).
+// CMPC_WIDE_FORM (A/B): 1 every class one-per-entry, 2 every class persistent.
+bool one_per_entry(int lo, int hi, int N, int batch) {
+  static const int form = [] {
+    const char* v = getenv("CMPC_WIDE_FORM");
+    return v ? atoi(v) : 0;
+  }();
+  if (form == 1 || batch < 16384) return true;
+  if (form == 2) return false;
+  const float mode = 6.f * (float)N, half = 3.f * sqrtf((float)N);
+  return (float)hi >= mode - half && (float)lo <= mode + half;
 }
 
 }  // namespace
@@ -79,12 +100,16 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   const bool split60 = (n_max <= 64) || (batch >= 16384);
   const int c1_nv = (n_max <= 60 || split60) ? 60 : 64;
   if (n_max > 64) {
-    hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_recs,
-                       batch, P, cnt, d_work + kHdr, max_batch, c1_nv);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the classify pass runs on side 0 beside class 1 (which needs no list: it skips the
+    // instances above its row width itself); side 1 waits for the lists
     if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
-    for (int s = 0; s < kSideStreams; s++)
-      if ((e = hipStreamWaitEvent(ctx.side[s], ctx.fork, 0)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(ctx.side[0], ctx.fork, 0)) != hipSuccess) return e;
+    hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 255) / 256), dim3(256), 0, ctx.side[0],
+                       d_recs, batch, P, cnt, d_work + kHdr, max_batch, c1_nv);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(ctx.classified, ctx.side[0])) != hipSuccess) return e;
+    for (int s = 1; s < kSideStreams; s++)
+      if ((e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
     int grid_of[kLists];
     for (int j = 0; j < kLists; j++) grid_of[j] = batch;
     // one workgroup per possible list entry (the lengths are only known on the device);
@@ -99,45 +124,44 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       static int* h_cnt = nullptr;
       if (!h_cnt && (e = hipHostMalloc(reinterpret_cast<void**>(&h_cnt), kHdr * sizeof(int))) != hipSuccess)
         return e;
-      if ((e = hipMemcpyAsync(h_cnt, cnt, kHdr * sizeof(int), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-          (e = hipStreamSynchronize(stream)) != hipSuccess)
+      if ((e = hipMemcpyAsync(h_cnt, cnt, kHdr * sizeof(int), hipMemcpyDeviceToHost, ctx.side[0])) != hipSuccess ||
+          (e = hipStreamSynchronize(ctx.side[0])) != hipSuccess)
         return e;
       for (int j = 0; j < kLists; j++) grid_of[j] = h_cnt[1 + j];
     }
+    // launch form per wide class (cmpc_wide.h): one workgroup per entry for the class that holds
+    // the trot size n = 6N, persistent workgroups (dequeue counter) for the others
+    auto dq = [&](int lst, int lo, int hi) -> int* {
+      return one_per_entry(lo, hi, P.N, batch) ? nullptr : &cnt[kDeq + lst];
+    };
     // the 64-wide class-1 build over its list (60 < n <= 64), ahead of the wide classes on side 1
     // (side 0 carries the 80 class, the longest chain at N = 10)
     if (split60 && (e = launch_class1(64, d_recs, batch, P, d_forces, d_status, d_iters, list[7],
                                       &cnt[8], nullptr, nullptr, grid_of[7], ctx.side[1])) != hipSuccess)
       return e;
-    // side 0: 80, 128, 256; side 1: 96, 144, 192 (at N = 20 the 128-column class and the
-    // 144/192-column classes, which carry the batch, run side by side)
-    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], &cnt[9 + 0], grid_of[0],
+    // side 0: 80, 120, 256; side 1: 96, 128, 144, 192, G (at N = 20 the 120-column class, which
+    // carries the batch, runs beside the 128/144/192-column classes)
+    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], dq(0, 65, 80), grid_of[0],
                              ctx.side[0])) != hipSuccess)
       return e;
-    if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], &cnt[9 + 1],
+    if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], dq(1, 81, 96),
                                            grid_of[1], ctx.side[1])) != hipSuccess)
       return e;
-    // CMPC_WIDE_ORDER=1 (A/B): the 144 class ahead of the 128 class on side 0 (longest solves
-    // first, no concurrent 128-class workgroups to starve its dispatch)
-    static const int order = [] {
-      const char* v = getenv("CMPC_WIDE_ORDER");
-      return v ? atoi(v) : 0;
-    }();
-    if (order == 1 && n_max > 128 &&
-        (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], &cnt[9 + 6], grid_of[6],
-                              ctx.side[0])) != hipSuccess)
+    // side 0: the 120-column build (every trot instance at N = 20); side 1: 121..128 and 144
+    if (n_max > 96 && (e = launch_wide_w120(d_recs, P, d_forces, d_status, d_iters, list[8], &cnt[9],
+                                            dq(8, 97, 120), grid_of[8], ctx.side[0])) != hipSuccess)
       return e;
-    if (n_max > 96 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3], &cnt[9 + 2],
-                                            grid_of[2], ctx.side[0])) != hipSuccess)
+    if (n_max > 120 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
+                                             dq(2, 121, 128), grid_of[2], ctx.side[1])) != hipSuccess)
       return e;
-    if (order != 1 && n_max > 128 &&
-        (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], &cnt[9 + 6], grid_of[6],
+    if (n_max > 128 &&
+        (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], &cnt[kDeq + 6], grid_of[6],
                               ctx.side[1])) != hipSuccess)
       return e;
-    if (n_max > 144 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4], &cnt[9 + 3],
+    if (n_max > 144 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4], &cnt[kDeq + 3],
                                              grid_of[3], ctx.side[1])) != hipSuccess)
       return e;
-    if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5], &cnt[9 + 4],
+    if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5], &cnt[kDeq + 4],
                                              grid_of[4], ctx.side[0])) != hipSuccess)
       return e;
     const bool g_possible = n_max > 256;
@@ -173,9 +197,19 @@ hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_f
   if (n <= 64)
     return launch_class1(n <= 60 ? 60 : 64, d_rec, 1, P, d_forces, d_status, d_iters, nullptr,
                          nullptr, nullptr, nullptr, 1, stream);
-  if (n <= 80) return launch_wide_w80(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
-  if (n <= 96) return launch_wide_w96(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
-  if (n <= 128) return launch_wide_w128(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
+  // the same kernel binary as the batched launch would use for this class (the two launch forms
+  // may round differently): the persistent form runs its loop once with deq == nullptr
+#define CMPC_SINGLE_WIDE(W, LO, HI)                                                                 \
+  if (n <= HI)                                                                                      \
+    return one_per_entry(LO, HI, P.N, 1)                                                            \
+               ? launch_wide_w##W(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream) \
+               : launch_wide_w##W##_persist(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, \
+                                            stream);
+  CMPC_SINGLE_WIDE(80, 65, 80)
+  CMPC_SINGLE_WIDE(96, 81, 96)
+  CMPC_SINGLE_WIDE(120, 97, 120)
+  CMPC_SINGLE_WIDE(128, 121, 128)
+#undef CMPC_SINGLE_WIDE
   if (n <= 144) return launch_wide_w144(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
   if (n <= 192) return launch_wide_w192(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
   if (n <= 256) return launch_wide_w256(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);

@@ -1,4 +1,4 @@
-// cmpc_wide.h — the wide size classes (template over the row width NV = 80, 96, 128, 192, 256):
+// cmpc_wide.h — the wide size classes (template over the row width NV = 80, 96, 120, 128, 144, 192, 256):
 // fused condensation + friction-cone QP for instances with more than 64 reduced force variables
 // (random contact tables at N = 10; trot at N >= 11, the deployed N = 16 and config 5's N = 20;
 // all-stance tables), over the classify pass's list of the class.
@@ -54,7 +54,7 @@ constexpr int kNoneW = 0x7fffffff;
 
 template <int NV>
 struct WGeo {
-  static_assert(NV % 16 == 0, "row width");
+  static_assert(NV % 8 == 0, "row width (each half's columns in 16-B chunks)");
   static constexpr int NH = NV / 2;             // columns per lane
   static constexpr int NW = (NV + 31) / 32;     // wavefronts (32 rows each)
   static constexpr int NT = 64 * NW;            // threads
@@ -909,18 +909,23 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
 
 }  // namespace
 
-// CMPC_WIDE_PERSIST (per width unit; on for the 144-, 192- and 256-column classes, whose
-// workgroups are the largest and the most often empty): persistent workgroups over the class's
-// list: as many as fit the GPU at this kernel's occupancy
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs, at most one per list slot), each dequeues
-// list entries with one global atomic until the list is exhausted. The list length is only known
-// on the device; a grid of one workgroup per possible entry made the GPU drain up to `batch` empty
-// workgroups per class (3.5 ms for the 146-KB workgroups of the 256 class at config 5, 1.2 ms for
-// the 192 class). With deq == nullptr (single-instance path) workgroup i takes entry i. The
-// persistent loop costs the 128 class 4 spilled VGPRs, so the populous classes keep one workgroup
-// per possible list entry.
-#ifndef CMPC_WIDE_PERSIST
-#define CMPC_WIDE_PERSIST 0
+// Two launch forms per class (CMPC_WIDE_BUILD per width unit: 1 one-per-entry, 2 persistent,
+// 3 both):
+//   * one workgroup per possible list entry (the list length is only known on the device);
+//     surplus workgroups exit after one load. No loop around the solve, so nothing is carried
+//     across instances. But an empty or sparse class drains up to `batch` empty workgroups: 3.5 ms
+//     for the one-per-CU 146-KB workgroups of the 256 class at config 5, 1.2 ms for the 192 class;
+//   * persistent: as many workgroups as fit the GPU at the kernel's occupancy
+//     (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs), each dequeuing list entries with one
+//     global atomic until the list is exhausted. The loop costs the populous classes registers
+//     (80 / 96 / 128: 11 / 20 / 4 spilled VGPRs).
+// launch_solve asks for the one-per-entry form (deq == nullptr) only for the class that holds the
+// trot size n = 6N (the mode of any contact mix: every instance at config 3 / N = 16 / N = 20
+// trot), the persistent form for every other class. The 144 / 192 / 256 classes are built
+// persistent only (no spills at their occupancy); their single-instance path runs the loop once
+// (deq == nullptr: workgroup i takes entry i).
+#ifndef CMPC_WIDE_BUILD
+#define CMPC_WIDE_BUILD 1
 #endif
 #if CMPC_WIDE_VGPR_CAP > 0
 #define CMPC_WIDE_VGPR_ATTR __attribute__((amdgpu_num_vgpr(CMPC_WIDE_VGPR_CAP)))
@@ -938,40 +943,39 @@ struct WideArgs {
   KParams P;
 };
 
-template <int NV>
+template <int NV, bool PERSIST>
 __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGPR_ATTR void cmpc_solve_w_kernel(
     WideArgs A) {
   __shared__ SharedW<NV> sh;
   const int count = *A.in_count;
-#if !CMPC_WIDE_PERSIST
-  {  // one workgroup per possible list entry
+  if constexpr (!PERSIST) {  // one workgroup per possible list entry
     const int b = blockIdx.x;
     if (b >= count) return;
     const int inst = A.in_list[b];
     solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
                 A.status + inst, A.iters ? A.iters + inst : nullptr);
+  } else {
+    for (int round = 0;; round++) {
+      // deq == nullptr (single-instance path): workgroup i takes entry i, once
+      if (threadIdx.x == 0) sh.deq_b = A.deq ? atomicAdd(A.deq, 1) : (round == 0 ? (int)blockIdx.x : count);
+      wbar();
+      const int b = __builtin_amdgcn_readfirstlane(sh.deq_b);
+      if (b >= count) break;
+      const int inst = A.in_list[b];
+      solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
+                  A.status + inst, A.iters ? A.iters + inst : nullptr);
+      wbar();  // every wave is done with this instance's LDS before the next record lands there
+    }
   }
-#else
-  for (int round = 0;; round++) {
-    // deq == nullptr (single-instance path): workgroup i takes entry i, once
-    if (threadIdx.x == 0) sh.deq_b = A.deq ? atomicAdd(A.deq, 1) : (round == 0 ? (int)blockIdx.x : count);
-    wbar();
-    const int b = __builtin_amdgcn_readfirstlane(sh.deq_b);
-    if (b >= count) break;
-    const int inst = A.in_list[b];
-    solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
-                A.status + inst, A.iters ? A.iters + inst : nullptr);
-    wbar();  // every wave is done with this instance's LDS before the next record lands there
-  }
-#endif
 }
 
-template <int NV>
+template <int NV, bool PERSIST>
 int wide_grid_cap() {
   static const int cap = [] {
     int nb = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc_solve_w_kernel<NV>, WGeo<NV>::NT, 0) !=
-            hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc_solve_w_kernel<NV, PERSIST>, WGeo<NV>::NT,
+                                                     0) != hipSuccess ||
+        nb <= 0)
       nb = 1;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
@@ -981,15 +985,30 @@ int wide_grid_cap() {
   return cap;
 }
 
+// deq != nullptr: persistent form (if built) with that dequeue counter; nullptr: one workgroup per
+// entry (if built; the persistent-only classes then run the loop once per workgroup). Internal
+// linkage: the width units compile it with different CMPC_WIDE_BUILD, and one shared
+// instantiation would serve both launch forms with whichever the linker kept.
+namespace {
 template <int NV>
 hipError_t launch_wide_impl(const float* d_recs, const KParams& P, float* d_forces,
                             uint8_t* d_status, int32_t* d_iters, const int* in_list,
                             const int* in_count, int* deq, int grid, hipStream_t stream) {
   if (grid <= 0) return hipSuccess;
-  if (CMPC_WIDE_PERSIST && deq) grid = grid < wide_grid_cap<NV>() ? grid : wide_grid_cap<NV>();
-  const WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, in_count, deq, P};
-  hipLaunchKernelGGL(cmpc_solve_w_kernel<NV>, dim3(grid), dim3(WGeo<NV>::NT), 0, stream, A);
+  constexpr bool kOne = (CMPC_WIDE_BUILD & 1) != 0, kPersist = (CMPC_WIDE_BUILD & 2) != 0;
+  const bool persist = kPersist && (deq != nullptr || !kOne);
+  WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, in_count, persist ? deq : nullptr, P};
+  if (persist) {
+    if constexpr (kPersist) {
+      if (deq) grid = grid < wide_grid_cap<NV, true>() ? grid : wide_grid_cap<NV, true>();
+      hipLaunchKernelGGL((cmpc_solve_w_kernel<NV, true>), dim3(grid), dim3(WGeo<NV>::NT), 0, stream, A);
+    }
+  } else {
+    if constexpr (kOne)
+      hipLaunchKernelGGL((cmpc_solve_w_kernel<NV, false>), dim3(grid), dim3(WGeo<NV>::NT), 0, stream, A);
+  }
   return hipGetLastError();
 }
+}  // namespace
 
 }  // namespace cmpc

@@ -4,7 +4,7 @@
 #ifndef CMPC_WIDE_WAVES_PER_EU
 #define CMPC_WIDE_WAVES_PER_EU 3
 #endif
-#define CMPC_WIDE_PERSIST 1  // persistent workgroups dequeue the list (cmpc_wide.h)
+#define CMPC_WIDE_BUILD 2  // launch forms built (cmpc_wide.h): persistent only
 #include "cmpc_wide.h"
 
 namespace cmpc {

@@ -1,5 +1,5 @@
 // cmpc_wide_w192.hip — wide size class with 192-column rows (kernel template: cmpc_wide.h).
-#define CMPC_WIDE_PERSIST 1  // persistent workgroups dequeue the list (cmpc_wide.h)
+#define CMPC_WIDE_BUILD 2  // launch forms built (cmpc_wide.h): persistent only
 #include "cmpc_wide.h"
 
 namespace cmpc {

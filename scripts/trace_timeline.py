@@ -10,9 +10,9 @@ import re
 
 
 def short(name):
-    m = re.search(r"cmpc_(\w+?)_kernel(<\d+>)?", name)
+    m = re.search(r"cmpc_(\w+?)_kernel(<[^>]*>)?", name)
     if m:
-        return m.group(1) + (m.group(2) or "")
+        return m.group(1) + (m.group(2) or "").replace(" ", "")
     return name.split("(")[0][-40:]
 
 
