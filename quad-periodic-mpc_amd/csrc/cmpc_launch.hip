@@ -100,15 +100,27 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   const bool split60 = (n_max <= 64) || (batch >= 16384);
   const int c1_nv = (n_max <= 60 || split60) ? 60 : 64;
   if (n_max > 64) {
-    // the classify pass runs on side 0 beside class 1 (which needs no list: it skips the
-    // instances above its row width itself); side 1 waits for the lists
-    if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(ctx.side[0], ctx.fork, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 255) / 256), dim3(256), 0, ctx.side[0],
+    // From 65536 instances the classify pass runs on side 0 beside class 1 (which needs no list:
+    // it skips the instances above its row width itself), side 1 waiting for the lists; below,
+    // on the handle's stream ahead of everything, so that the wide classes (the critical path of
+    // a small batch) start as early as they can. Same-box A/B (profiles/r03_ab/r03_h): config 3
+    // +1.7 % with classify beside class 1, batch 32768 -4.6 %, config 2 -1.5 %.
+    // CMPC_CLASSIFY_SIDE=0/1 forces either placement (A/B).
+    static const int cls_env = [] {
+      const char* v = getenv("CMPC_CLASSIFY_SIDE");
+      return v ? atoi(v) : -1;
+    }();
+    const bool cls_side = (cls_env < 0) ? (batch >= 65536) : (cls_env == 1);
+    hipStream_t cs = cls_side ? ctx.side[0] : stream;
+    if (cls_side) {
+      if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(ctx.side[0], ctx.fork, 0)) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 255) / 256), dim3(256), 0, cs,
                        d_recs, batch, P, cnt, d_work + kHdr, max_batch, c1_nv);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipEventRecord(ctx.classified, ctx.side[0])) != hipSuccess) return e;
-    for (int s = 1; s < kSideStreams; s++)
+    if ((e = hipEventRecord(ctx.classified, cs)) != hipSuccess) return e;
+    for (int s = cls_side ? 1 : 0; s < kSideStreams; s++)
       if ((e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
     int grid_of[kLists];
     for (int j = 0; j < kLists; j++) grid_of[j] = batch;
@@ -124,8 +136,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       static int* h_cnt = nullptr;
       if (!h_cnt && (e = hipHostMalloc(reinterpret_cast<void**>(&h_cnt), kHdr * sizeof(int))) != hipSuccess)
         return e;
-      if ((e = hipMemcpyAsync(h_cnt, cnt, kHdr * sizeof(int), hipMemcpyDeviceToHost, ctx.side[0])) != hipSuccess ||
-          (e = hipStreamSynchronize(ctx.side[0])) != hipSuccess)
+      if ((e = hipMemcpyAsync(h_cnt, cnt, kHdr * sizeof(int), hipMemcpyDeviceToHost, cs)) != hipSuccess ||
+          (e = hipStreamSynchronize(cs)) != hipSuccess)
         return e;
       for (int j = 0; j < kLists; j++) grid_of[j] = h_cnt[1 + j];
     }

@@ -27,11 +27,12 @@ for setting in default "$@"; do
   if [ "$setting" = default ]; then envp=""; else envp="env $setting"; fi
   step c3_$tag 300 $envp $B --steps 30 || exit 1
   step c2_$tag 300 $envp $B --config 2 --steps 200 || exit 1
+  step c3h_$tag 300 $envp $B --batch 32768 --steps 30 || exit 1
   step n16_$tag 300 $envp $B --horizon 16 --random-contact-frac 0 --steps 10 --warmup 2 || exit 1
   step n20_$tag 300 $envp $B --horizon 20 --random-contact-frac 0 --steps 10 --warmup 2 || exit 1
   step c5_$tag 300 $envp $B --config 5 --steps 10 --warmup 2 || exit 1
 done
-for f in "$OUT"/c3_* "$OUT"/c2_* "$OUT"/n16_* "$OUT"/n20_* "$OUT"/c5_*; do ms "$f"; done
+for f in "$OUT"/c3_* "$OUT"/c3h_* "$OUT"/c2_* "$OUT"/n16_* "$OUT"/n20_* "$OUT"/c5_*; do ms "$f"; done
 if [ "${PROF:-1}" = 1 ]; then
   step rocprof_c5 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- python3 bench.py --config 5 --no-cpu-baseline --no-extras --steps 5 --warmup 2 || exit 1
   f=$(find "$OUT/prof_c5" -name "*kernel_trace.csv" | head -n 1)
