@@ -1,5 +1,5 @@
 #!/bin/bash
-# N = 20 trot phase split of the w128 class: default library vs diagnostic variants that stop
+# N = 20 trot phase split of the w120 class (n = 120 trot): default library vs diagnostic variants that stop
 # after the Cholesky (diag1) and after J = L^-T (diag2). Timing only (results of the variants
 # are not solutions).
 set -u
