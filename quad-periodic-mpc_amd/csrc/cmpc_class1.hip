@@ -114,6 +114,11 @@ struct SharedC1 {
   static_assert(NV * (NV + 1) / 2 <= C1Geo<NV>::PSZ, "R must fit in P");
   static_assert(OFF_REC + CMPC_REC_WORDS(MAXN) <= C1Geo<NV>::PSZ, "prep scratch must fit in P");
   static_assert(3 * C1_MAXFS >= NV, "stance list");
+  // the broadcast vector (y, then the masked d / Householder vector) lives in P's last NL words
+  // once J is formed: the factor rows are dead, and R (at most NV (NV + 1) / 2 words) stays below
+  // it. 256 B less: the 64-wide build fits 10 KB, i.e. 16 workgroups per CU (it had 15)
+  static_assert(NV * (NV + 1) / 2 <= C1Geo<NV>::PSZ - NL, "vbuf in P's tail");
+  __device__ __forceinline__ float* vbuf() { return &P[C1Geo<NV>::PSZ - NL]; }
   float P[C1Geo<NV>::PSZ];
   // arrays of different stages share one region: 10 KB of LDS per instance at NV = 60, so
   // sixteen one-wave workgroups (four waves per SIMD) fit a CU's 160 KB
@@ -122,16 +127,14 @@ struct SharedC1 {
     float ibuf[NL];        // Cholesky + J: 1 / sqrt(d_k) of pivot k
     struct {               // active set
       float bufA[NL], bufB[NL];  // published J rows ia, iz (contiguous: bufA[NL + c] = bufB[c])
-      float xs[NL];
       float cs[2 * NL];    // Givens (c, s) per column pair
     } gi;
   } u;
-  float vbuf[NL];          // broadcast vector (y, then masked d)
   float sub[C1_MAXFS];     // ub of each stance foot-step (gait * f_max)
   int sfs[C1_MAXFS];       // stance foot-step ids, in order
   int blkbase[MAXN + 2];   // first reduced variable of each horizon step
   unsigned char varblk[NL], varcol[NL];
-  unsigned char cflag[2 * NL + 8];  // active flag per constraint id (6 per stance foot-step)
+  unsigned char cmask[NL];  // active flags of stance foot-step s's 6 constraints (bit t of byte s)
 };
 
 __device__ __forceinline__ void lsync() {
@@ -228,7 +231,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       const unsigned long long hi = (b1 <= 0) ? 0ull : (msk1 & ((1ull << b1) - 1ull));
       sh.blkbase[v] = 3 * (__popcll(lo) + __popcll(hi));
     }
-    for (int t = v; t < 6 * nfs; t += 64) sh.cflag[t] = 0;
+    for (int t = v; t < nfs; t += 64) sh.cmask[t] = 0;
   }
   Model md;
   make_model(srec, P.dt, md);
@@ -512,11 +515,11 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 
   C1_MARK(3);
   // ---- unconstrained minimiser x = -J y ----------------------------------------------------
-  sh.vbuf[v] = yv;
+  sh.vbuf()[v] = yv;
   lsync();
   f2v xacc = {0.f, 0.f};
   piped_sweep<0, NV, C1_PIPE_GRP>(
-      [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf[decltype(C)::value]); },
+      [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf()[decltype(C)::value]); },
       [&](auto C, float4 y4) {
         constexpr int c = decltype(C)::value;
         dot4(xacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], y4);
@@ -549,12 +552,12 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       t_sub = clock64();
 #endif
       if (p < 0) {
-        sh.u.gi.xs[v] = xv;
-        lsync();
+        // foot-step v's forces from lanes 3v .. 3v+2 by ds_bpermute (no LDS store + reload)
+        const float fx = __shfl(xv, 3 * v), fy = __shfl(xv, 3 * v + 1), fz = __shfl(xv, 3 * v + 2);
         float best = 0.f;
         int bid = 0x7fffffff;
         if (v < nfs) {
-          const float fx = sh.u.gi.xs[3 * v], fy = sh.u.gi.xs[3 * v + 1], fz = sh.u.gi.xs[3 * v + 2];
+          const unsigned fm = sh.cmask[v];
           float sl[6];
           sl[0] = (mui * fx + fz) * fnorm;
           sl[1] = (-mui * fx + fz) * fnorm;
@@ -564,7 +567,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           sl[5] = sh.sub[v] - fz;
 #pragma unroll
           for (int t = 0; t < 6; t++)
-            if (!sh.cflag[6 * v + t] && sl[t] < best) { best = sl[t]; bid = 6 * v + t; }
+            if (!((fm >> t) & 1u) && sl[t] < best) { best = sl[t]; bid = 6 * v + t; }
         }
         const float xmax = wave_max(fabsf(xv));
         wave_argmin(best, bid);
@@ -589,12 +592,12 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       lsync();
       const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.u.gi.bufA[v], cp.cb * sh.u.gi.bufB[v]) : cp.cb * sh.u.gi.bufB[v];
       const float dm = (v >= q && v < n) ? dv : 0.f;
-      sh.vbuf[v] = dm;
+      sh.vbuf()[v] = dm;
       lsync();
       // z = J2 d2 (primal step direction), zn = |d2|^2 = z' n+, dn = |d|^2
       f2v zacc = {0.f, 0.f}, nacc = {0.f, 0.f};
       piped_sweep<0, NV, C1_PIPE_GRP>(
-          [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf[decltype(C)::value]); },
+          [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf()[decltype(C)::value]); },
           [&](auto C, float4 m4) {
             constexpr int c = decltype(C)::value;
             dot4(zacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], m4);
@@ -652,7 +655,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         const float dq = rl(dv, q);
         const float sgn = (dq >= 0.f) ? 1.f : -1.f;
         beta = fast_rcp(ts * (ts + fabsf(dq)));  // 2 / (w'w)
-        sh.vbuf[v] = (v == q) ? dq + sgn * ts : dm;
+        sh.vbuf()[v] = (v == q) ? dq + sgn * ts : dm;
         const int offq = rcol(q);
         if (v < q) sh.P[offq + v] = dv;
         if (v == q) {
@@ -660,15 +663,15 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           u_reg = up;
           act_reg = p;
         }
-        if (v == 0) sh.cflag[p] = 1;
+        if (v == 0) sh.cmask[p / 6] |= (unsigned char)(1u << (p % 6));
       } else {
         // ---- drop active constraint kk: shift positions kk+1..q-1 down, remove column kk of
         // R and re-triangularise rows kk..q-1 (lane c rebuilds column c of R in place: every
         // read of an old entry precedes, in this wavefront's LDS order, the write reusing it)
-        sh.vbuf[v] = 0.f;
+        sh.vbuf()[v] = 0.f;
         const int k = __builtin_amdgcn_readfirstlane(kk);
         const int ak = rli(act_reg, k);
-        if (v == 0) sh.cflag[ak] = 0;
+        if (v == 0) sh.cmask[ak / 6] &= (unsigned char)~(1u << (ak % 6));
         const int a_nx = lane_next_i(act_reg, act_reg);
         const float u_nx = lane_next(u_reg, u_reg);
         if (v >= k && v < q - 1) { act_reg = a_nx; u_reg = u_nx; }
@@ -707,7 +710,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         // J <- J (I - beta w w'): tw = J_v . w, J_v -= beta tw w  (no-op on a drop: beta = 0)
         f2v tacc = {0.f, 0.f};
         piped_sweep<0, NV, C1_PIPE_GRP>(
-            [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf[decltype(C)::value]); },
+            [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf()[decltype(C)::value]); },
             [&](auto C, float4 w4) {
               constexpr int c = decltype(C)::value;
               dot4(tacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], w4);
@@ -717,7 +720,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         // sweep's loads live for the second (a whole row of extra VGPRs)
         asm volatile("" ::: "memory");
         piped_sweep<0, NV, C1_PIPE_GRP>(
-            [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf[decltype(C)::value]); },
+            [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf()[decltype(C)::value]); },
             [&](auto C, float4 w4) {
               constexpr int c = decltype(C)::value;
               axpy4(bt, w4, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3]);

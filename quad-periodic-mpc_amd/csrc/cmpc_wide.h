@@ -675,6 +675,39 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
           acc[m] = (lane + 64 * m < NV) ? sh.dfull()[(lane + 64 * m) < NV ? lane + 64 * m : 0] : 0.f;
           r_a[m] = 0.f;
         }
+#if CMPC_WIDE_WAVES_PER_EU <= 4
+        // software-pipelined: the LDS reads of step i - 1 are issued before step i's chain (the
+        // five-waves-per-SIMD builds keep the plain loop: 96 VGPRs leave no room for it)
+        float pd = 1.f, pv[RQ];
+#pragma unroll
+        for (int m = 0; m < RQ; m++) pv[m] = 0.f;
+        if (q > 0) {
+          const int off = rcol_w(q - 1);
+          pd = sh.P[off + q - 1];
+#pragma unroll
+          for (int m = 0; m < RQ; m++) pv[m] = (lane + 64 * m < q - 1) ? sh.P[off + lane + 64 * m] : 0.f;
+        }
+        for (int i = q - 1; i >= 0; i--) {
+          float pd_n = 1.f, pv_n[RQ];
+#pragma unroll
+          for (int m = 0; m < RQ; m++) pv_n[m] = 0.f;
+          if (i > 0) {
+            const int offn = rcol_w(i - 1);
+            pd_n = sh.P[offn + i - 1];
+#pragma unroll
+            for (int m = 0; m < RQ; m++) pv_n[m] = (lane + 64 * m < i - 1) ? sh.P[offn + lane + 64 * m] : 0.f;
+          }
+          const float ri = wdiv(rl_pos<RQ>(acc, i), pd);
+#pragma unroll
+          for (int m = 0; m < RQ; m++) {
+            const int pos = lane + 64 * m;
+            if (pos < i) acc[m] = fmaf(-pv[m], ri, acc[m]);
+            r_a[m] = (pos == i) ? ri : r_a[m];
+            pv[m] = pv_n[m];
+          }
+          pd = pd_n;
+        }
+#else
         for (int i = q - 1; i >= 0; i--) {
           const int off = rcol_w(i);
           const float ri = wdiv(rl_pos<RQ>(acc, i), sh.P[off + i]);
@@ -685,6 +718,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
             r_a[m] = (pos == i) ? ri : r_a[m];
           }
         }
+#endif
         float t1w = kBigF;
         int kw = kNoneW;
 #pragma unroll
