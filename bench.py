@@ -361,7 +361,8 @@ def scaling_model(args, cm, dev, sync):
     rows, t1 = [], None
     for G in (1, 2, 4, 8):
         local = G_total // G
-        pipe = par.RootPipeline(prm, local, device=dev)
+        # the pieces a G-rank run cuts each rank's shard into (world 1 itself solves in one piece)
+        pipe = par.RootPipeline(prm, local, chunks=par.auto_chunks(local, G), device=dev)
         recs = recs_all[:local]
         for _ in range(3):
             pipe.step(recs)

@@ -98,6 +98,12 @@ struct C1Geo {
 };
 // R (upper triangular, q x q) packed by columns: R[i][j] at rcol(j) + i, i <= j
 __device__ __forceinline__ int rcol(int j) { return (j * (j + 1)) >> 1; }
+// largest q whose two packed triangles fit in `words`
+constexpr int rinv_cols(int words) {
+  int q = 0;
+  while ((q + 1) * (q + 2) <= words) q++;
+  return q;
+}
 
 // prep scratch inside P (P is not yet holding H while these are live)
 constexpr int OFF_E = 0;
@@ -119,6 +125,11 @@ struct SharedC1 {
   // it. 256 B less: the 64-wide build fits 10 KB, i.e. 16 workgroups per CU (it had 15)
   static_assert(NV * (NV + 1) / 2 <= C1Geo<NV>::PSZ - NL, "vbuf in P's tail");
   __device__ __forceinline__ float* vbuf() { return &P[C1Geo<NV>::PSZ - NL]; }
+  // R^-1 (active-set phase, while the active set has at most QI positions and nothing was
+  // dropped): packed by columns like R, below vbuf; R's first QI columns stay below it
+  static constexpr int QI = rinv_cols(C1Geo<NV>::PSZ - NL);
+  static constexpr int RB = C1Geo<NV>::PSZ - NL - QI * (QI + 1) / 2;
+  static_assert(QI * (QI + 1) / 2 <= RB, "R and R^-1 side by side");
   float P[C1Geo<NV>::PSZ];
   // arrays of different stages share one region: 10 KB of LDS per instance at NV = 60, so
   // sixteen one-wave workgroups (four waves per SIMD) fit a CU's 160 KB
@@ -543,6 +554,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   int p = -1;          // constraint being added (-1: pick the most violated one)
   Cons cp{};
   float up = 0.f;
+  bool rinv_ok = true;  // R^-1 kept beside R (wave-uniform)
   lsync();
   if (status == CMPC_OK) {
     for (;;) {
@@ -609,10 +621,29 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       asm volatile("" : "+v"(zv), "+v"(zn));
       const float dn = wave_sum((v < n) ? dv * dv : 0.f);
       C1_SUB(1);
-      // r = R^-1 d1: back substitution over the packed columns of R (lane i ends with r_i)
-      // (software-pipelined: the LDS reads of step i - 1 are issued before step i's chain)
+      // r = R^-1 d1 (lane i ends with r_i). While R^-1 is kept (every step so far an add, q <=
+      // QI) it is a matvec over its packed columns: no dependent chain, four columns per trip.
+      // Otherwise a back substitution over the packed columns of R, software-pipelined (the LDS
+      // reads of step i - 1 are issued before step i's readlane / divide / FMA chain).
       float acc = dv, r_reg = 0.f;
-      {
+      if (rinv_ok) {
+        using S = SharedC1<NV>;
+        float a0 = 0.f, a1 = 0.f;
+        int j = 0;
+        for (; j + 4 <= q; j += 4) {
+          const float x0 = sh.P[S::RB + rcol(j) + v], x1 = sh.P[S::RB + rcol(j + 1) + v];
+          const float x2 = sh.P[S::RB + rcol(j + 2) + v], x3 = sh.P[S::RB + rcol(j + 3) + v];
+          a0 = fmaf((v <= j) ? x0 : 0.f, rl(dv, j), a0);
+          a1 = fmaf((v <= j + 1) ? x1 : 0.f, rl(dv, j + 1), a1);
+          a0 = fmaf((v <= j + 2) ? x2 : 0.f, rl(dv, j + 2), a0);
+          a1 = fmaf((v <= j + 3) ? x3 : 0.f, rl(dv, j + 3), a1);
+        }
+        for (; j < q; j++) {
+          const float x0 = sh.P[S::RB + rcol(j) + v];
+          a0 = fmaf((v <= j) ? x0 : 0.f, rl(dv, j), a0);
+        }
+        r_reg = (v < q) ? a0 + a1 : 0.f;
+      } else {
         float pd = 1.f, pv = 0.f;
         if (q > 0) {
           pd = sh.P[rcol(q - 1) + q - 1];
@@ -663,12 +694,24 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           u_reg = up;
           act_reg = p;
         }
+        // R^-1 gains the column (-r / rho, 1 / rho), rho = R's new diagonal: [R d1; 0 rho]^-1
+        if (rinv_ok) {
+          if (q < SharedC1<NV>::QI) {
+            const float irho = 1.f / (-sgn * ts);
+            const int offi = SharedC1<NV>::RB + rcol(q);
+            if (v < q) sh.P[offi + v] = -r_reg * irho;
+            if (v == q) sh.P[offi + q] = irho;
+          } else {
+            rinv_ok = false;
+          }
+        }
         if (v == 0) sh.cmask[p / 6] |= (unsigned char)(1u << (p % 6));
       } else {
         // ---- drop active constraint kk: shift positions kk+1..q-1 down, remove column kk of
         // R and re-triangularise rows kk..q-1 (lane c rebuilds column c of R in place: every
         // read of an old entry precedes, in this wavefront's LDS order, the write reusing it)
         sh.vbuf()[v] = 0.f;
+        rinv_ok = false;  // R^-1 is not updated through a drop: back substitution from here on
         const int k = __builtin_amdgcn_readfirstlane(kk);
         const int ak = rli(act_reg, k);
         if (v == 0) sh.cmask[ak / 6] &= (unsigned char)~(1u << (ak % 6));
