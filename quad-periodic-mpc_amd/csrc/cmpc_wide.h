@@ -91,7 +91,11 @@ struct WGeo {
   static constexpr int O_VBUF = PSZ_R, O_BUFA = O_VBUF + VL, O_BUFB = O_BUFA + VL;
   static constexpr int O_DFULL = O_BUFB + VL, O_XS = O_DFULL + NV, O_CS = O_XS + NV;
   static constexpr int GI_END = O_CS + 2 * NV + 8;
-  static constexpr int PTOT = (mx(mx(PSZ + 12 * 16, PSZ + CH), GI_END) + 3) & ~3;
+  // R^-1 beside R for the first QI active-set positions (sized to keep each class's workgroups
+  // per CU: 80 / 96 six, 120 / 128 four)
+  static constexpr int QI = (NV == 80) ? 56 : (NV == 96) ? 40 : (NV == 120) ? 48 : (NV == 128) ? 32 : 64;
+  static constexpr int O_RINV = (GI_END + 3) & ~3;
+  static constexpr int PTOT = (mx(mx(PSZ + 12 * 16, PSZ + CH), O_RINV + QI * (QI + 1) / 2) + 3) & ~3;
   static_assert(PSZ % 4 == 0 && PSZ_R % 4 == 0 && VL % 4 == 0, "16-B aligned stage buffers");
 };
 
@@ -576,6 +580,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   const float mui = P.mu_inv;
   const float fnorm = rsqrtf(mui * mui + 1.f);
   int q = 0;
+  bool rinv_ok = true;  // R^-1 kept beside R (wave-uniform)
   int iters = 0;
   float u_a[RQ], r_a[RQ];
   int a_a[RQ];
@@ -668,7 +673,40 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         for (int w = 0; w < G::NW; w++) dn += sh.redf[w];
       }
       // r = R^-1 d1 by back substitution (wave 0), then the dual step t1 = min u_j / r_j
-      if (wave == 0) {
+      if (wave == 0 && rinv_ok) {
+        // R^-1 kept (only adds so far, q <= QI): r = R^-1 d1 as a matvec, four columns per trip
+        float ra[RQ];
+#pragma unroll
+        for (int m = 0; m < RQ; m++) ra[m] = 0.f;
+        int j = 0;
+        for (; j + 4 <= q; j += 4) {
+          const float4 d4 = *reinterpret_cast<const float4*>(&sh.dfull()[j]);
+          const float dj[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const int off = G::O_RINV + rcol_w(j + e);
+#pragma unroll
+            for (int m = 0; m < RQ; m++) {
+              const int pos = lane + 64 * m;
+              const float x = sh.P[off + ((pos <= j + e) ? pos : j + e)];
+              ra[m] = fmaf((pos <= j + e) ? x : 0.f, dj[e], ra[m]);
+            }
+          }
+        }
+        for (; j < q; j++) {
+          const int off = G::O_RINV + rcol_w(j);
+          const float dj = sh.dfull()[j];
+#pragma unroll
+          for (int m = 0; m < RQ; m++) {
+            const int pos = lane + 64 * m;
+            const float x = sh.P[off + ((pos <= j) ? pos : j)];
+            ra[m] = fmaf((pos <= j) ? x : 0.f, dj, ra[m]);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < RQ; m++) r_a[m] = (lane + 64 * m < q) ? ra[m] : 0.f;
+      }
+      if (wave == 0 && !rinv_ok) {
         float acc[RQ];
 #pragma unroll
         for (int m = 0; m < RQ; m++) {
@@ -719,6 +757,8 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
           }
         }
 #endif
+      }
+      if (wave == 0) {
         float t1w = kBigF;
         int kw = kNoneW;
 #pragma unroll
@@ -758,22 +798,31 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         beta = fast_rcp(ts * (ts + fabsf(dq)));  // 2 / (w'w)
         if (t < NV) {
           sh.vbuf()[lidx<NV>(t)] = (t == q) ? dq + sgn * ts : dm;
-          *reinterpret_cast<float2*>(&sh.cs()[2 * t + (t >= NH ? 4 : 0)]) = make_float2(1.f, 0.f);
           const int offq = rcol_w(q);
           if (t < q) sh.P[offq + t] = dv;
           if (t == q) sh.P[offq + q] = -sgn * ts;
         }
         if (wave == 0) {
+          // R^-1 gains the column (-r / rho, 1 / rho), rho = R's new diagonal
+          const bool keep = rinv_ok && q < G::QI;
+          const float irho = 1.f / (-sgn * ts);
+          const int offi = G::O_RINV + rcol_w(q);
 #pragma unroll
-          for (int m = 0; m < RQ; m++)
+          for (int m = 0; m < RQ; m++) {
+            const int pos = lane + 64 * m;
             if (lane + 64 * m == q) { u_a[m] = up; a_a[m] = p; }
+            if (keep && pos < q) sh.P[offi + pos] = -r_a[m] * irho;
+            if (keep && pos == q) sh.P[offi + q] = irho;
+          }
         }
+        if (q >= G::QI) rinv_ok = false;
         if (t == 0) sh.cflag[p] = 1;
       } else {
         // ---- drop active constraint kk: shift positions kk+1..q-1 down, remove column kk of R,
         // re-triangularise rows kk..q-1 with Givens rotations (wave 0, in place)
         const int k = kk;
         seam = (q > NH);
+        rinv_ok = false;  // R^-1 is not updated through a drop: back substitution from here on
         if (t < NV) {
           sh.vbuf()[lidx<NV>(t)] = 0.f;
           if (t < k || t > q - 2)
