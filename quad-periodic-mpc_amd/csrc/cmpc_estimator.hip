@@ -40,7 +40,7 @@ constexpr int NTAPS7 = 2 * kGaussR7 + 1, NTAPS27 = 2 * kGaussR27 + 1;
 static_assert(W % NOUT == 0 && NFIR <= NT && NBIN <= 2 * NT, "estimator thread mapping");
 
 struct SharedE {
-  double d[W];       // window, oldest first
+  double d[W + W / 8];  // window, oldest first, one pad slot per 8 samples (dslot)
   double band[W];    // blur7 - blur27
   double k7[NTAPS7], k27[NTAPS27];
   double redd[NWV];
@@ -62,18 +62,23 @@ __device__ __forceinline__ double block_sum_d(double x, SharedE& sh) {
   return s;
 }
 
+// LDS slot of window sample i: one pad slot per 8 samples. Thread t reads samples 4t + c, 32 B
+// apart: unpadded, a 32-lane group of ds_read_b64 hit 8 bank pairs (4-way conflicts, 1.33 extra
+// LDS cycles per LDS instruction in the counters); padded, the pairs spread over the 64 banks
+__device__ __forceinline__ int dslot(int i) { return i + (i >> 3); }
+
 // one Gaussian FIR over outputs i0..i0+3, edge-clamped, taps ascending (SolverMPC.cpp:419-436)
 template <int R>
 __device__ __forceinline__ void fir4(const double* __restrict__ d, const double* __restrict__ k,
                                      int i0, double (&acc)[NOUT]) {
   double win[NOUT];
 #pragma unroll
-  for (int r = 0; r < NOUT - 1; r++) win[r + 1] = d[min(max(i0 - R + r, 0), W - 1)];
+  for (int r = 0; r < NOUT - 1; r++) win[r + 1] = d[dslot(min(max(i0 - R + r, 0), W - 1))];
 #pragma unroll 8
   for (int j = -R; j <= R; j++) {
 #pragma unroll
     for (int r = 0; r < NOUT - 1; r++) win[r] = win[r + 1];
-    win[NOUT - 1] = d[min(max(i0 + j + NOUT - 1, 0), W - 1)];
+    win[NOUT - 1] = d[dslot(min(max(i0 + j + NOUT - 1, 0), W - 1))];
     const double kj = k[j + R];
 #pragma unroll
     for (int r = 0; r < NOUT; r++) acc[r] = fma(win[r], kj, acc[r]);
@@ -179,7 +184,7 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
   double* prm = reinterpret_cast<double*>(st + CMPC_EST_PARAMS);  // stat, amp, freq, phase
   if (count >= W && count <= CMPC_EST_STOP) {
     const int head = sh.head;
-    for (int i = tid; i < W; i += NT) sh.d[i] = (double)st[CMPC_EST_F + (head + i) % W];
+    for (int i = tid; i < W; i += NT) sh.d[dslot(i)] = (double)st[CMPC_EST_F + (head + i) % W];
     for (int i = tid; i < NTAPS7; i += NT) sh.k7[i] = (double)gauss[i];  // float taps, exact
     for (int i = tid; i < NTAPS27; i += NT) sh.k27[i] = (double)gauss[NTAPS7 + i];
     if (tid == 0) {

@@ -127,6 +127,37 @@ def test_random_batches_match_reference_live(cm, orc, solver_mod, N, stress, fra
     assert_parity(orc, recs, prm, f, q, ok, label=f"live stress={stress} frac={frac}")
 
 
+CLASS_EDGES = [0, 60, 64, 80, 96, 120, 128, 144, 192, 256]  # class 1 (60 / 64 builds), wide 80 .. 256
+
+
+@pytest.mark.parametrize("N", [10, 16, 20])
+def test_large_batch_every_size_class_live(cm, orc, solver_mod, N):
+    """A batch >= 16384 (the size from which the sparse wide classes launch as persistent
+    workgroups and the populous ones one workgroup per entry, cmpc_launch.hip one_per_entry) with
+    random contact tables, so every size class and both launch forms run; up to 40 instances of
+    each class are checked against the reference pipeline run live."""
+    if not orc.ref_available():
+        pytest.skip("oracle/_ref not present")
+    prm = cm.make_params(N)
+    B = 16384
+    recs = cm.make_instances(B, N, seed=8100 + N, random_contact_frac=1.0)
+    n = 3 * (cm.unpack_gait(recs, N) != 0).sum(1)
+    f, st, it = gpu_solve(solver_mod, prm, recs)
+    rng = np.random.default_rng(N)
+    pick, seen = [], []
+    for lo, hi in zip(CLASS_EDGES[:-1], CLASS_EDGES[1:]):
+        idx = np.nonzero((n > lo) & (n <= hi))[0]
+        if idx.size:
+            seen.append(f"{lo + 1}-{hi}:{idx.size}")
+            pick.append(rng.choice(idx, min(40, idx.size), replace=False))
+    sel = np.concatenate(pick)
+    print(f"[classes] N={N} batch {B}: " + " ".join(seen))
+    q, st_ref, _ = orc.ref_solve_batch(recs[sel], prm, nthreads=16)
+    ok = st_ref == 0
+    assert (st[sel][ok] == 0).all()
+    assert_parity(orc, recs[sel], prm, f[sel], q, ok, label=f"every class B={B}")
+
+
 def test_device_path_deterministic(cm, solver_mod):
     import torch
     prm = cm.make_params(10)
