@@ -102,17 +102,16 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   const bool split60 = (n_max <= 64) || (batch >= 16384);
   const int c1_nv = (n_max <= 60 || split60) ? 60 : 64;
   if (n_max > 64) {
-    // From 65536 instances the classify pass runs on side 0 beside class 1 (which needs no list:
+    // From 16384 instances the classify pass runs on side 0 beside class 1 (which needs no list:
     // it skips the instances above its row width itself), side 1 waiting for the lists; below,
-    // on the handle's stream ahead of everything, so that the wide classes (the critical path of
-    // a small batch) start as early as they can. Same-box A/B (profiles/r03_ab/r03_h): config 3
-    // +1.7 % with classify beside class 1, batch 32768 -4.6 %, config 2 -1.5 %.
-    // CMPC_CLASSIFY_SIDE=0/1 forces either placement (A/B).
+    // on the handle's stream ahead of everything. Batch sweep of both placements with the final
+    // kernels (profiles/r03_ab/sweep2): beside class 1 +2 % at 16384 .. 131072 instances, within
+    // noise below. CMPC_CLASSIFY_SIDE=0/1 forces either placement (A/B).
     static const int cls_env = [] {
       const char* v = getenv("CMPC_CLASSIFY_SIDE");
       return v ? atoi(v) : -1;
     }();
-    const bool cls_side = (cls_env < 0) ? (batch >= 65536) : (cls_env == 1);
+    const bool cls_side = (cls_env < 0) ? (batch >= 16384) : (cls_env == 1);
     hipStream_t cs = cls_side ? ctx.side[0] : stream;
     if (cls_side) {
       if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;

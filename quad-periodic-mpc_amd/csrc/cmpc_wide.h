@@ -383,6 +383,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   // published into P's row k (even / odd segments), one s_barrier per step
   int status = CMPC_OK;
   float my_inv = 1.f;
+#if CMPC_DIAG_STOP != 3  // diagnostic build 3: stop after the condensation and the H-row load
 #if CMPC_WIDE_CHOL2
   // Two pivots per step (k even, k+1: register k/2 of half 0 and of half 1 of every row), one
   // s_barrier per step instead of per pivot. Each lane publishes its own pivot column entry
@@ -474,6 +475,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     }
   });
 #endif
+#endif  // CMPC_DIAG_STOP != 3
   float yv;
   {
     CMPC_WIDE_IDS();
@@ -482,7 +484,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   }
   wbar();
 
-#if CMPC_DIAG_STOP != 1  // diagnostic builds: stop after the Cholesky (1) / after J (2)
+#if CMPC_DIAG_STOP != 1 && CMPC_DIAG_STOP != 3  // diagnostic builds: stop after the Cholesky (1) / after J (2)
   // ---- J = L^-T: row r solves L x = e_r over its half of the columns (LDS reads only; the
   // pivot value x_k lives in the half holding column k: one partner exchange per step)
   {
