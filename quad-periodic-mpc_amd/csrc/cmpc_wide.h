@@ -43,6 +43,10 @@
 #ifndef CMPC_WIDE_J2
 #define CMPC_WIDE_J2 CMPC_WIDE_CHOL2
 #endif
+// wavefronts skip the factorisation steps that cannot change their rows (1); 0: every wave sweeps
+#ifndef CMPC_WIDE_SKIP
+#define CMPC_WIDE_SKIP 1
+#endif
 #ifndef CMPC_WIDE_VGPR_CAP
 #define CMPC_WIDE_VGPR_CAP 0
 #endif
@@ -429,17 +433,21 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       const float s1 = fmaf(-hk, beta, hk1);
       const float a1 = (r > k1 && r < NV) ? -s1 * (i1 * i1) : 0.f;
       const float a0 = (r > k && r < NV) ? fmaf(-a1, beta, -hk * (i0 * i0)) : 0.f;
-      const float* prow0 = &sh.P[base + h * st - j0];
-      const float* prow1 = &sh.P[base1 + h * st - j0];
+      // a wavefront whose rows are all factored (r <= k) or all padding (r >= n) has a0 = a1 = 0:
+      // it skips the sweep (scalar branch; 20 % of the sweep reads at NV = 120, more with more waves)
+      if (CMPC_WIDE_SKIP == 0 || (32 * wave + 31 > k && 32 * wave < n)) {
+        const float* prow0 = &sh.P[base + h * st - j0];
+        const float* prow1 = &sh.P[base1 + h * st - j0];
 #pragma unroll
-      for (int j = j0; j < NH; j += 4) {
-        const float4 r0 = *reinterpret_cast<const float4*>(prow0 + j);
-        const float4 r1 = *reinterpret_cast<const float4*>(prow1 + j);
-        axpy4(a0, r0, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
-        axpy4(a1, r1, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
-        CMPC_WSWEEP2_FENCE(j);
+        for (int j = j0; j < NH; j += 4) {
+          const float4 r0 = *reinterpret_cast<const float4*>(prow0 + j);
+          const float4 r1 = *reinterpret_cast<const float4*>(prow1 + j);
+          axpy4(a0, r0, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+          axpy4(a1, r1, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3]);
+          CMPC_WSWEEP2_FENCE(j);
+        }
+        gb = fmaf(a1, g1, fmaf(a0, g0, gb));
       }
-      gb = fmaf(a1, g1, fmaf(a0, g0, gb));
       wpin(slot);
     }
   });
@@ -506,7 +514,9 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     constexpr int j0 = G::j0(k);
     constexpr int base = G::fbase(k), base1 = G::fbase(k1);
     constexpr int st = G::seg(k);
-    if (k < n) {
+    // rows r > k + 1 have x_k = x_k+1 = 0 (L is lower triangular): a wavefront whose rows all lie
+    // past the pivot pair skips the step (its slot k stays the +0 the step would store)
+    if (k < n && (CMPC_WIDE_SKIP == 0 || k1 >= 32 * wave)) {
       wlsync();
       const int h = (lane_opq() >> 5) & 1;
       const float i0 = sh.ibuf()[k], i1 = sh.ibuf()[k1];
