@@ -340,6 +340,8 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     float z[13];
 #pragma unroll
     for (int j = 0; j < 13; j++) z[j] = 0.f;
+    // (stopping each wavefront below the smallest block of its rows, whose steps build nothing,
+    // measured 0.5-1 % slower on every workload: profiles/r03_ab/r03_o)
     for (int i = N - 1; i >= 0; i--) {
       // z_i = S Adt^{i-kv} b_r + Adt' z_{i+1}  (the S term only for i >= kv)
       const bool act = real && (i >= kv);

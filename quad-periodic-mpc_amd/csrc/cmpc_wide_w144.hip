@@ -1,6 +1,6 @@
 // cmpc_wide_w144.hip — wide size class with 144-column rows (n 129-144: random contact tables at N = 20) (kernel template: cmpc_wide.h).
-// two waves per SIMD: at three the 72-column half rows spill (25 VGPRs); five waves per
-// workgroup, 52 KB of LDS
+// three waves per SIMD (166 VGPRs, no VGPR spills; capped at 128 the compiler keeps 166), five
+// waves per workgroup, 55 KB of LDS: two workgroups per CU
 #ifndef CMPC_WIDE_WAVES_PER_EU
 #define CMPC_WIDE_WAVES_PER_EU 3
 #endif
