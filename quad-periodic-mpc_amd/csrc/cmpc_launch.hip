@@ -152,8 +152,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if (split60 && (e = launch_class1(64, d_recs, batch, P, d_forces, d_status, d_iters, list[7],
                                       &cnt[8], nullptr, nullptr, grid_of[7], ctx.side[1])) != hipSuccess)
       return e;
-    // side 0: 80, 120, 256; side 1: 96, 128, 144, 192, G (at N = 20 the 120-column class, which
-    // carries the batch, runs beside the 128/144/192-column classes)
+    // side 0: 80, 120, 144, 256; side 1: 96, 128, 192, G (at N = 20 the 120-column class, which
+    // carries the batch, runs beside the 128-column class)
     if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], dq(0, 65, 80), grid_of[0],
                              ctx.side[0])) != hipSuccess)
       return e;
@@ -167,12 +167,21 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if (n_max > 120 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
                                              dq(2, 121, 128), grid_of[2], ctx.side[1])) != hipSuccess)
       return e;
+    // The 144 class on side 0 behind the 120 class, the 192 class on side 1 behind the 128 class:
+    // at N = 20 the two sparse classes then start as soon as either bulk class drains and run side
+    // by side instead of back to back. Config 5 4.21 M -> 4.41 M QP/s against both on side 1
+    // (profiles/r03_ab/sparse_side). CMPC_SPARSE_SIDE (A/B): the side streams of the 144 / 192
+    // classes as two digits (11 = both on side 1)
+    static const int sparse_side = [] {
+      const char* v = getenv("CMPC_SPARSE_SIDE");
+      return v ? atoi(v) : 1;
+    }();
     if (n_max > 128 &&
         (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], &cnt[kDeq + 6], grid_of[6],
-                              ctx.side[1])) != hipSuccess)
+                              ctx.side[(sparse_side / 10) & 1])) != hipSuccess)
       return e;
     if (n_max > 144 && (e = launch_wide_w192(d_recs, P, d_forces, d_status, d_iters, list[3], &cnt[4], &cnt[kDeq + 3],
-                                             grid_of[3], ctx.side[1])) != hipSuccess)
+                                             grid_of[3], ctx.side[sparse_side % 10 & 1])) != hipSuccess)
       return e;
     if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5], &cnt[kDeq + 4],
                                              grid_of[4], ctx.side[0])) != hipSuccess)
