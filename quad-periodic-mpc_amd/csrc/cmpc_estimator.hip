@@ -39,10 +39,27 @@ constexpr int NFIR = W / NOUT;
 constexpr int NTAPS7 = 2 * kGaussR7 + 1, NTAPS27 = 2 * kGaussR27 + 1;
 static_assert(W % NOUT == 0 && NFIR <= NT && NBIN <= 2 * NT, "estimator thread mapping");
 
+// DFT of the band: 0 = mixed-radix Stockham FFT (radices 4, 4, 5, 5) in LDS; 1 = one Goertzel
+// recurrence per bin (the round-2 form, 200 x 400 dependent fp64 steps per instance)
+#ifndef CMPC_EST_GOERTZEL
+#define CMPC_EST_GOERTZEL 0
+#endif
+static_assert(W == 400, "the FFT's radix plan is 4 * 4 * 5 * 5");
+constexpr int QW = W / 4;  // quarter-period twiddle table
+
 struct SharedE {
-  double d[W + W / 8];  // window, oldest first, one pad slot per 8 samples (dslot)
-  double band[W];    // blur7 - blur27
-  double k7[NTAPS7], k27[NTAPS27];
+  union {
+    struct {
+      double d[W + W / 8];  // window, oldest first, one pad slot per 8 samples (dslot)
+      double k7[NTAPS7], k27[NTAPS27];
+    } fir;
+    double2 fa[W];  // FFT stages 1 / 3 output (the FIR's inputs are dead by then)
+  };
+  union {
+    double band[W];  // blur7 - blur27
+    double2 fb[W];   // FFT stages 2 / 4 output (the band is dead after stage 1)
+  };
+  double2 tw[QW];  // e^{-2 pi i m / W}, m < W / 4 (the other quarters by symmetry)
   double redd[NWV];
   int redi[NWV];
   int count, head;
@@ -82,6 +99,57 @@ __device__ __forceinline__ void fir4(const double* __restrict__ d, const double*
     const double kj = k[j + R];
 #pragma unroll
     for (int r = 0; r < NOUT; r++) acc[r] = fma(win[r], kj, acc[r]);
+  }
+}
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+// e^{-2 pi i k / W}, 0 <= k < W, from the quarter table: e^{-i pi q / 2} = (-i)^q
+__device__ __forceinline__ double2 twid(const double2* __restrict__ T, int k) {
+  const int q = k / QW, m = k - QW * q;
+  const double2 t = T[m];
+  return (q == 0) ? t : (q == 1) ? make_double2(t.y, -t.x) : (q == 2) ? make_double2(-t.x, -t.y)
+                                                                        : make_double2(-t.y, t.x);
+}
+// one Stockham autosort stage of radix R over sub-transforms of length NS (NS = product of the
+// earlier radices): thread j < W / R twiddles its R inputs in[j + r W/R] by e^{-2 pi i (j % NS) r /
+// (NS R)}, takes their length-R DFT and writes out[(j / NS) NS R + j % NS + m NS]. The band enters
+// stage 1 as real input (REAL_IN)
+template <int R, int NS, bool REAL_IN>
+__device__ __forceinline__ void fft_stage(const double2* __restrict__ in, const double* __restrict__ in_re,
+                                          double2* __restrict__ out, const double2* __restrict__ T, int j) {
+  constexpr int M = W / R;
+  if (j >= M) return;
+  const int k = j % NS;
+  double2 v[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    double2 x = REAL_IN ? make_double2(in_re[j + r * M], 0.0) : in[j + r * M];
+    if (NS > 1 && r > 0) x = cmul(x, twid(T, (k * r * (W / (NS * R))) % W));
+    v[r] = x;
+  }
+  const int d = (j / NS) * NS * R + k;
+#pragma unroll
+  for (int m = 0; m < R; m++) {
+    double2 acc = v[0];
+#pragma unroll
+    for (int r = 1; r < R; r++) {
+      const int e = (r * m) % R;
+      if (e == 0) {
+        acc.x += v[r].x; acc.y += v[r].y;
+      } else if (R == 4 && e == 2) {  // -1
+        acc.x -= v[r].x; acc.y -= v[r].y;
+      } else if (R == 4 && e == 1) {  // -i
+        acc.x += v[r].y; acc.y -= v[r].x;
+      } else if (R == 4 && e == 3) {  // +i
+        acc.x -= v[r].y; acc.y += v[r].x;
+      } else {
+        const double2 c = cmul(v[r], twid(T, e * (W / R)));
+        acc.x += c.x; acc.y += c.y;
+      }
+    }
+    out[d + m * NS] = acc;
   }
 }
 
@@ -184,9 +252,16 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
   double* prm = reinterpret_cast<double*>(st + CMPC_EST_PARAMS);  // stat, amp, freq, phase
   if (count >= W && count <= CMPC_EST_STOP) {
     const int head = sh.head;
-    for (int i = tid; i < W; i += NT) sh.d[dslot(i)] = (double)st[CMPC_EST_F + (head + i) % W];
-    for (int i = tid; i < NTAPS7; i += NT) sh.k7[i] = (double)gauss[i];  // float taps, exact
-    for (int i = tid; i < NTAPS27; i += NT) sh.k27[i] = (double)gauss[NTAPS7 + i];
+    for (int i = tid; i < W; i += NT) sh.fir.d[dslot(i)] = (double)st[CMPC_EST_F + (head + i) % W];
+    for (int i = tid; i < NTAPS7; i += NT) sh.fir.k7[i] = (double)gauss[i];  // float taps, exact
+    for (int i = tid; i < NTAPS27; i += NT) sh.fir.k27[i] = (double)gauss[NTAPS7 + i];
+#if !CMPC_EST_GOERTZEL
+    if (tid < QW) {
+      double sn, cs;
+      sincospi(2.0 * tid / W, &sn, &cs);
+      sh.tw[tid] = make_double2(cs, -sn);
+    }
+#endif
     if (tid == 0) {
       sh.t0 = st[CMPC_EST_T + head];
       sh.t1 = st[CMPC_EST_T + (head + 1) % W];
@@ -196,8 +271,8 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
     if (tid < NFIR) {
       const int i0 = NOUT * tid;
       double a7[NOUT] = {0.0, 0.0, 0.0, 0.0}, a27[NOUT] = {0.0, 0.0, 0.0, 0.0};
-      fir4<kGaussR7>(sh.d, sh.k7, i0, a7);
-      fir4<kGaussR27>(sh.d, sh.k27, i0, a27);
+      fir4<kGaussR7>(sh.fir.d, sh.fir.k7, i0, a7);
+      fir4<kGaussR27>(sh.fir.d, sh.fir.k27, i0, a27);
 #pragma unroll
       for (int r = 0; r < NOUT; r++) sh.band[i0 + r] = a7[r] - a27[r];
     }
@@ -209,9 +284,28 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
     part = 0.0;
     for (int i = tid; i < W; i += NT) part += (sh.band[i] - mean) * (sh.band[i] - mean);
     const double sd = sqrt(block_sum_d(part, sh) / W);
-    // |DFT|^2 of bins tid+1 and tid+101 by Goertzel recurrences
     double v = __builtin_huge_val();
     int bi = 0x7fffffff;
+#if !CMPC_EST_GOERTZEL
+    // |DFT|^2 of bins tid+1 and tid+101 from a 400-point FFT of the band (4 stages, a barrier
+    // each; the reference's rfft, SolverMPC.cpp:503, agrees to ~1e-13 relative on the magnitudes)
+    fft_stage<4, 1, true>(nullptr, sh.band, sh.fa, sh.tw, tid);
+    __syncthreads();
+    fft_stage<4, 4, false>(sh.fa, nullptr, sh.fb, sh.tw, tid);
+    __syncthreads();
+    fft_stage<5, 16, false>(sh.fb, nullptr, sh.fa, sh.tw, tid);
+    __syncthreads();
+    fft_stage<5, 80, false>(sh.fa, nullptr, sh.fb, sh.tw, tid);
+    __syncthreads();
+    if (tid < NBIN / 2) {
+      const int ka = tid + 1, kb = tid + 1 + NBIN / 2;
+      const double2 xa = sh.fb[ka], xb = sh.fb[kb];
+      const double ma = xa.x * xa.x + xa.y * xa.y;
+      const double mb = xb.x * xb.x + xb.y * xb.y;
+      if (mb > ma) { v = -mb; bi = kb; } else { v = -ma; bi = ka; }
+    }
+#else
+    // |DFT|^2 of bins tid+1 and tid+101 by Goertzel recurrences
     if (tid < NBIN / 2) {
       const int ka = tid + 1, kb = tid + 1 + NBIN / 2;
       double ca, sa, cb, sb;
@@ -239,6 +333,7 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
       // the larger magnitude, ties to the smaller bin (negated for the min-reduction)
       if (mb > ma) { v = -mb; bi = kb; } else { v = -ma; bi = ka; }
     }
+#endif
     // first maximum: reduce on (-|X|^2, k)
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
