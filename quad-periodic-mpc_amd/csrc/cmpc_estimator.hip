@@ -17,11 +17,12 @@
 //     widened to double in LDS). Per tap one LDS read extends a 4-sample sliding window in
 //     registers and feeds four fp64 FMAs; taps are accumulated in ascending order per output,
 //     as gaussian_filter does;
-//   * DFT peak: thread t < 100 runs the Goertzel recurrence s = x + 2 cos(w) s1 - s2 for bins
-//     t+1 and t+101 over the band (one broadcast LDS read per two samples, no twiddle gathers:
-//     the round-1 kernel's table lookups at (k t) mod 400 were 1.8 bank conflicts per LDS
-//     instruction), |X_k|^2 = s1^2 + s2^2 - 2 cos(w) s1 s2; the first maximum over bins 1..200
-//     (a direct DFT or the reference's FFT agree to ~1e-12 relative on the magnitudes);
+//   * DFT peak: a 400-point Stockham FFT of the band in LDS (radices 4, 4, 5, 5; twiddles from a
+//     quarter-period table of 100 sincospi values, the other quarters by symmetry), then thread
+//     t < 100 takes |X_k|^2 of bins t+1 and t+101; the first maximum over bins 1..200 (the
+//     reference's rfft agrees to ~1e-13 relative on the magnitudes). Round 2's 200 Goertzel
+//     recurrences (400 dependent fp64 steps each) stay behind -DCMPC_EST_GOERTZEL=1: the FFT cut
+//     the launch from 1.03 to 0.75 ms at config 5;
 //   * mean / std / argmax: wave butterflies plus one LDS exchange.
 // Instances outside the estimation window only push their sample (a few words of HBM traffic)
 // and evaluate the compensation.
