@@ -279,6 +279,17 @@ def local_leg(args, cm, prm, config, N, B, steps, warmup, dev, rank, barrier, sy
                 recs=recs, recs_np=recs_np, world=world)
 
 
+WIDE_CLASS_NV = (80, 96, 120, 128, 144, 192, 256)   # row widths of the wide classes (cmpc_wide.h)
+
+
+def carrying_wide_kernel(N: int) -> str:
+    """Kernel name of the wide class that holds the trot size n = 6 N (every instance of the
+    trot workloads, the mode of any contact mix): launched one workgroup per list entry
+    (cmpc_launch.hip one_per_entry), hence the `false` (not persistent) template argument."""
+    nv = next(v for v in WIDE_CLASS_NV if v >= 6 * N)
+    return f"cmpc_solve_w_kernel<{nv}, false>"
+
+
 def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
     """roofline object of the dominant launch (see the module docstring / DESIGN.md §5)."""
     if not launch_ms.size:
@@ -297,7 +308,7 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
     # class 1 runs as the 60-wide build once the batch fills the GPU (>= 16384 instances at
     # N >= 6, cmpc_launch.hip), else as the 64-wide build
     c1w = 60 if (units_per_launch >= 16384 or N <= 5) else 64
-    wide_k = f"cmpc_solve_w_kernel<{96 if N <= 16 else 128}>"   # the class that carries the batch
+    wide_k = carrying_wide_kernel(N)
     traffic, pmc = load_pmc(N, units_per_launch, f"cmpc_solve_c1_kernel<{c1w}>" if not wide
                             else wide_k)
     roofline = {

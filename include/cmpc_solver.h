@@ -188,6 +188,14 @@ void update_x_drag(float x_drag);
  * definitions take precedence. f_ext has Eigen::Matrix<float,6,1> layout (6 floats). */
 CMPC_EXTERNC float f_ext[6];
 CMPC_EXTERNC float simulation_time;
+/* The solver's own estimator globals (SolverMPC.h:72-74, SolverMPC.cpp:390-392, 772-798):
+ * f_est(3) = the compensation force of the last update_problem_data* call (fed into qg once more
+ * than 500 samples were pushed), f_est_smoothed = 0.95 f_est_smoothed + 0.05 f_est, and
+ * f_est_static(3) = 0.97 f_est_static(3) + 0.03 f_ext(3). Eigen::Matrix<float,6,1> layout. The
+ * estimator step itself runs on the device (the kernel of cmpc_batch_estimate, one instance). */
+CMPC_EXTERNC float f_est[6];
+CMPC_EXTERNC float f_est_smoothed[6];
+CMPC_EXTERNC float f_est_static[6];
 
 /* ------------------------------------------------------------------------------------------ */
 /* 2. Batched, reentrant API                                                                   */
@@ -225,7 +233,10 @@ typedef struct cmpc_admm_settings {
  * cmpc_batch_condense, A = fmat, l = 0, u = U_b) solved by JCQP's ADMM in fp64, one workgroup
  * per instance, any horizon. With s->reduced (use_jcqp == 2, SolverMPC.cpp:984-1053) the swing
  * legs are eliminated first. QPs of up to 120 variables keep the inverted KKT Schur complement in
- * LDS; larger ones in per-workgroup global slabs allocated with the handle. d_forces
+ * LDS; larger ones (N > 10) in per-workgroup fp64 global slabs (min(max_batch, 512) x (12N)^2
+ * doubles: 151 MB at N = 16, 236 MB at N = 20), allocated by the handle's FIRST cmpc_batch_admm
+ * call and kept from then on (handles that never run ADMM never pay for them): make that first
+ * call outside stream capture, and expect an allocation failure to surface there. d_forces
  * [batch * 12N] = the solution as float (0 for eliminated variables); d_status 0 = residual
  * below terminate, 1 = max_iter reached; d_iters (may be NULL). */
 CMPC_EXTERNC int cmpc_batch_admm(cmpc_batch* h, const float* d_records, const float* d_H,

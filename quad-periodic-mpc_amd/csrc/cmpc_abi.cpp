@@ -353,7 +353,8 @@ static int ensure_staging(cmpc_batch* h) {
   const int one[2] = {1, 0};
   hipError_t e;
   const char* what = "hipMalloc";
-  if ((e = hipMalloc(&h->d_rec, words * sizeof(float))) == hipSuccess &&
+  // d_rec: 4 words past the last record for the single-instance ABI's (f_ext[3], simulation_time)
+  if ((e = hipMalloc(&h->d_rec, (words + 4) * sizeof(float))) == hipSuccess &&
       (e = hipMalloc(&h->d_forces, (size_t)12 * CMPC_MAX_HORIZON * h->max_batch * sizeof(float))) == hipSuccess &&
       (e = hipMalloc(&h->d_status, (size_t)h->max_batch)) == hipSuccess &&
       (e = hipMalloc(&h->d_iters, sizeof(int32_t) * h->max_batch)) == hipSuccess &&
@@ -362,7 +363,7 @@ static int ensure_staging(cmpc_batch* h) {
       (e = hipMalloc(&h->d_single_out, (12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) == hipSuccess &&
       (what = "hipHostMalloc",
        e = hipHostMalloc(reinterpret_cast<void**>(&h->h_pin),
-                         (CMPC_REC_WORDS(CMPC_MAX_HORIZON) + 12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) == hipSuccess &&
+                         (CMPC_REC_WORDS(CMPC_MAX_HORIZON) + 4 + 12 * CMPC_MAX_HORIZON + 4) * sizeof(float))) == hipSuccess &&
       (what = "H2D", e = hipMemcpy(h->d_one, one, sizeof(one), hipMemcpyHostToDevice)) == hipSuccess) {
     h->staged = true;
     return 0;
@@ -390,7 +391,7 @@ static int solve_single_host(cmpc_batch* h, const float* record, float* forces, 
   const size_t rw = (size_t)CMPC_REC_WORDS(N);
   const int n = host_reduced_size(record, N, h->prm.f_max);
   float* pin_rec = h->h_pin;
-  float* pin_out = h->h_pin + CMPC_REC_WORDS(CMPC_MAX_HORIZON);
+  float* pin_out = h->h_pin + CMPC_REC_WORDS(CMPC_MAX_HORIZON) + 4;
   std::memcpy(pin_rec, record, rw * sizeof(float));
   float* d_out = h->d_single_out;
   uint8_t* d_st = reinterpret_cast<uint8_t*>(d_out + 12 * N);
@@ -443,6 +444,11 @@ extern "C" {
 // weak here so the library also loads on its own. The host program's definitions win.
 __attribute__((weak)) float f_ext[6] = {0, 0, 0, 0, 0, 0};
 __attribute__((weak)) float simulation_time = 0.f;
+// The solver's own globals (SolverMPC.h:72-74, SolverMPC.cpp:390-392; Eigen::Matrix<float,6,1>
+// layout): the compensation force of the last call and its two smoothed copies
+float f_est[6] = {0, 0, 0, 0, 0, 0};
+float f_est_smoothed[6] = {0, 0, 0, 0, 0, 0};
+float f_est_static[6] = {0, 0, 0, 0, 0, 0};
 }
 
 namespace {
@@ -463,133 +469,36 @@ struct SingleState {
   int has_solved = 0;
   cmpc_batch* h = nullptr;
   int h_horizon = -1;
-  // periodic-disturbance estimator state (SolverMPC.cpp:390-398, 555-563, 688-798)
-  std::vector<float> time_history, diff_history;
-  double est_stat = 0, est_amp = 0, est_freq = 0, est_phase = 0;
-  float f_est[6]{}, f_est_smoothed[6]{}, f_est_static[6]{};
+  // periodic-disturbance estimator state (SolverMPC.cpp:390-398, 555-563, 688-798): histories,
+  // count and fit on the device (cmpc_estimator.hip ring of the last 400 samples); f_est,
+  // f_est_smoothed and f_est_static are the exported globals below
+  float* d_est = nullptr;
 };
 SingleState g;
 
-// gaussian_filter (SolverMPC.cpp:404-437): float kernel, radius ceil(3 sigma), edge clamp
-std::vector<double> gaussian_filter(const std::vector<double>& data, float sigma) {
-  const int radius = (int)std::ceil(3 * sigma);
-  std::vector<float> kernel(2 * radius + 1);
-  float sum = 0.0;
-  for (int i = -radius; i <= radius; i++) {
-    const float value = std::exp(-0.5 * (i * i) / (sigma * sigma));
-    kernel[i + radius] = value;
-    sum += value;
+// The estimator state of the single-instance ABI lives on the device (one CMPC_EST_WORDS slot,
+// cmpc_estimator.hip): the same kernel as the batched config-5 path runs the reference's per-call
+// estimator step (SolverMPC.cpp:688-798) ahead of the solve, so one implementation serves both.
+int ensure_single_est(SingleState& s) {
+  if (s.d_est) return 0;
+  hipError_t e = hipMalloc(&s.d_est, CMPC_EST_WORDS * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(s.d_est, 0, CMPC_EST_WORDS * sizeof(float));
+  if (e != hipSuccess) {
+    if (s.d_est) (void)hipFree(s.d_est);
+    s.d_est = nullptr;
+    return fail("hipMalloc(estimator state)", e);
   }
-  for (auto& k : kernel) k /= sum;
-  const int n = (int)data.size();
-  std::vector<double> out(n, 0.0);
-  for (int i = 0; i < n; i++) {
-    double acc = 0.0;
-    for (int j = -radius; j <= radius; j++) {
-      int idx = i + j;
-      idx = idx < 0 ? 0 : (idx >= n ? n - 1 : idx);
-      acc += data[idx] * kernel[j + radius];
-    }
-    out[i] = acc;
-  }
-  return out;
+  return 0;
 }
 
-// Mixed-radix decimation-in-time DFT, in place (the reference calls FFTW's r2c here): data[0..n)
-// with twiddles tw[j] = exp(-2 pi i j / N) of the top-level size N, stride_tw = N / n, and a
-// scratch of n. Prime factors beyond the smallest split are done directly.
-void fft_mixed(std::complex<double>* data, int n, int stride_tw, const std::vector<std::complex<double>>& tw,
-               std::complex<double>* scratch) {
-  if (n == 1) return;
-  const int N = (int)tw.size();
-  int p = 2;
-  while (n % p) p++;
-  if (p == n) {  // prime length: direct
-    for (int k = 0; k < n; k++) {
-      std::complex<double> acc(0, 0);
-      for (int t = 0; t < n; t++) acc += data[t] * tw[((long)stride_tw * k * t) % N];
-      scratch[k] = acc;
-    }
-    for (int k = 0; k < n; k++) data[k] = scratch[k];
-    return;
-  }
-  const int m = n / p;
-  for (int r = 0; r < p; r++)
-    for (int j = 0; j < m; j++) scratch[r * m + j] = data[j * p + r];
-  for (int r = 0; r < p; r++) fft_mixed(scratch + r * m, m, stride_tw * p, tw, data + r * m);
-  for (int k = 0; k < m; k++)
-    for (int q = 0; q < p; q++) {
-      std::complex<double> acc(0, 0);
-      for (int r = 0; r < p; r++) acc += scratch[r * m + k] * tw[((long)stride_tw * r * (k + q * m)) % N];
-      data[k + q * m] = acc;
-    }
-}
-
-// fit_sin initial guesses (SolverMPC.cpp:478-541): peak |rfft| bin >= 1, amp = sqrt2 std,
-// offset = mean, phase = 0. The r2c magnitudes come from a mixed-radix FFT (400 = 2^4 5^2).
-void fit_sin(const std::vector<double>& tt, const std::vector<double>& yy, double& amp,
-             double& freq, double& phase, double& offset) {
-  const int n = (int)tt.size();
-  const double dt = tt[1] - tt[0];
-  std::vector<std::complex<double>> tw(n), X(n), scratch(n);
-  for (int j = 0; j < n; j++) tw[j] = std::polar(1.0, -2.0 * M_PI * (double)j / (double)n);
-  for (int t = 0; t < n; t++) X[t] = std::complex<double>(yy[t], 0.0);
-  fft_mixed(X.data(), n, 1, tw, scratch.data());
-  int best = 1;
-  double best_mag = -1.0;
-  for (int k = 1; k <= n / 2; k++) {
-    const double mag = std::abs(X[k]);
-    if (k == 1 || mag > best_mag) { best_mag = mag; best = k; }
-  }
-  const double f = (best <= n / 2) ? best / (n * dt) : (best - n) / (n * dt);
-  double m = 0;
-  for (double y : yy) m += y;
-  m /= n;
-  double s = 0;
-  for (double y : yy) s += (y - m) * (y - m);
-  s = std::sqrt(s / n);
-  amp = s * std::sqrt(2.0);
-  offset = m;
-  phase = 0.0;
-  freq = (2 * M_PI * std::fabs(f)) / (2 * M_PI);
-}
-
-void estimator_step(SingleState& s) {
-  // SolverMPC.cpp:692-798
-  s.diff_history.push_back(f_ext[3]);
-  s.time_history.push_back(simulation_time);
-  const size_t window = 400;
-  if (s.time_history.size() >= window) {
-    if (s.time_history.size() <= 500) {
-      std::vector<double> tw(s.time_history.end() - window, s.time_history.end());
-      std::vector<double> dw(s.diff_history.end() - window, s.diff_history.end());
-      auto blurred = gaussian_filter(dw, 7.0f);
-      auto very_blurred = gaussian_filter(dw, 27.0f);
-      std::vector<double> band(dw.size());
-      for (size_t i = 0; i < dw.size(); i++) band[i] = blurred[i] - very_blurred[i];
-      fit_sin(tw, band, s.est_amp, s.est_freq, s.est_phase, s.est_stat);
-    }
-    // NB: '+' as in the reference (SolverMPC.cpp:766)
-    const float comp = (float)(s.est_amp + std::sin(2 * M_PI * simulation_time * s.est_freq + s.est_phase));
-    s.f_est[3] = comp;
-  }
-  for (int i = 0; i < 6; i++) s.f_est_smoothed[i] = 0.95f * s.f_est_smoothed[i] + 0.05f * s.f_est[i];
-  s.f_est_static[3] = 0.97f * s.f_est_static[3] + 0.03f * f_ext[3];
-}
-
-// One instance through condense + ADMM on the handle's stream (host record in, host forces out).
-int admm_host(cmpc_batch* h, const float* rec, int N, const cmpc_admm_settings& as, float* forces,
-              uint8_t* st) {
-  if (int r = ensure_staging(h)) return r;
+// One instance through condense + ADMM on the handle's stream; the record is already in h->d_rec
+// (staged with the estimator step), host forces out.
+int admm_device(cmpc_batch* h, int N, const cmpc_admm_settings& as, float* forces, uint8_t* st) {
   const size_t n = 12 * (size_t)N;
   float* dH = h->d_admm_H;
   float* dg = dH + n * n;
   hipError_t e;
-  int rc = 0;
-  if ((e = hipMemcpyAsync(h->d_rec, rec, CMPC_REC_WORDS(N) * sizeof(float), hipMemcpyHostToDevice,
-                          h->stream)) != hipSuccess)
-    rc = fail("H2D", e);
-  if (!rc) rc = cmpc_batch_condense(h, h->d_rec, 1, dH, dg);
+  int rc = cmpc_batch_condense(h, h->d_rec, 1, dH, dg);
   if (!rc) rc = cmpc_batch_admm(h, h->d_rec, dH, dg, 1, &as, h->d_forces, h->d_status, nullptr);
   if (!rc && (e = hipMemcpyAsync(forces, h->d_forces, n * sizeof(float), hipMemcpyDeviceToHost,
                                  h->stream)) != hipSuccess)
@@ -598,6 +507,59 @@ int admm_host(cmpc_batch* h, const float* rec, int N, const cmpc_admm_settings& 
     rc = fail("D2H", e);
   if (!rc && (e = hipStreamSynchronize(h->stream)) != hipSuccess) rc = fail("sync", e);
   return rc;
+}
+
+// One solve_mpc call (SolverMPC.cpp:566-1089) of the single-instance ABI on the batch-1 handle:
+// one H2D of the record with (f_ext[3], simulation_time) behind it, the estimator step on the
+// device (writes f_est(3) and the use-f_est flag into the device record), then exactly one
+// solver kernel of the record's size class (launch_single) or, for use_jcqp, condense + ADMM; one
+// D2H of forces, status word and f_est(3).
+int solve_single_device(SingleState& s, const float* rec, int N, float* forces, uint8_t* st) {
+  cmpc_batch* h = s.h;
+  if (int r = ensure_staging(h)) return r;
+  if (int r = ensure_single_est(s)) return r;
+  const size_t rw = (size_t)CMPC_REC_WORDS(N);
+  float* pin_rec = h->h_pin;
+  float* pin_out = h->h_pin + CMPC_REC_WORDS(CMPC_MAX_HORIZON) + 4;
+  std::memcpy(pin_rec, rec, rw * sizeof(float));
+  pin_rec[rw] = f_ext[3];            // diff_history.push_back(f_ext(3))  (SolverMPC.cpp:692)
+  pin_rec[rw + 1] = simulation_time; // time_history.push_back(simulation_time)  (:698)
+  float* d_out = h->d_single_out;    // [forces 12N][status word][f_est(3)]
+  uint8_t* d_st = reinterpret_cast<uint8_t*>(d_out + 12 * N);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(h->d_rec, pin_rec, (rw + 2) * sizeof(float), hipMemcpyHostToDevice, h->stream)) !=
+      hipSuccess)
+    return fail("H2D", e);
+  if ((e = cmpc::launch_estimate(s.d_est, nullptr, h->d_rec + rw, h->d_rec + rw + 1, 0.f, h->d_rec, (int)rw,
+                                 nullptr, h->d_gauss, 1, h->stream, d_out + 12 * N + 1)) != hipSuccess)
+    return fail("launch_estimate", e);
+  if (s.use_jcqp == 1 || s.use_jcqp == 2) {
+    // use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): ADMM over the full QP; use_jcqp == 2
+    // (:984-1053): over the reduced one; any horizon (QPs beyond 120 variables keep M^-1 in a
+    // global slab)
+    cmpc_admm_settings as{s.max_iterations, s.rho, s.sigma, s.solver_alpha, s.terminate,
+                          s.use_jcqp == 2 ? 1 : 0};
+    if (int r = admm_device(h, N, as, forces, st)) return r;
+    if ((e = hipMemcpy(&f_est[3], d_out + 12 * N + 1, sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess)
+      return fail("D2H", e);
+    return 0;
+  }
+  const int n = host_reduced_size(rec, N, h->prm.f_max);
+  if (n <= 256) {
+    e = cmpc::launch_single(h->d_rec, n, h->kp, d_out, d_st, h->d_iters, h->d_one, h->d_gscratch, h->stream);
+  } else {  // class G: its slabs and list through the batched launch sequence
+    if (int r = cmpc_batch_solve(h, h->d_rec, 1, d_out, d_st, nullptr)) return r;
+    e = hipSuccess;
+  }
+  if (e != hipSuccess) return fail("launch_single", e);
+  if ((e = hipMemcpyAsync(pin_out, d_out, (12 * N + 2) * sizeof(float), hipMemcpyDeviceToHost, h->stream)) !=
+      hipSuccess)
+    return fail("D2H", e);
+  if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail("sync", e);
+  std::memcpy(forces, pin_out, 12 * N * sizeof(float));
+  std::memcpy(st, pin_out + 12 * N, 1);
+  std::memcpy(&f_est[3], pin_out + 12 * N + 1, sizeof(float));
+  return 0;
 }
 
 void solve_single(SingleState& s) {
@@ -624,8 +586,7 @@ void solve_single(SingleState& s) {
     return;
   }
 
-  estimator_step(s);
-
+  // the record; f_est(3) and the use-f_est flag are written by the device estimator step
   std::vector<float> rec(CMPC_REC_WORDS(N), 0.f);
   std::memcpy(&rec[CMPC_REC_P], s.p, sizeof(s.p));
   std::memcpy(&rec[CMPC_REC_V], s.v, sizeof(s.v));
@@ -636,39 +597,25 @@ void solve_single(SingleState& s) {
   rec[CMPC_REC_RPY + 1] = s.pitch;
   rec[CMPC_REC_RPY + 2] = s.yaw;
   rec[CMPC_REC_XDRAG] = s.x_drag;
-  rec[CMPC_REC_FEST3] = s.f_est[3];
-  const uint32_t flags = (s.time_history.size() > 500) ? 1u : 0u;  // SolverMPC.cpp:808
-  std::memcpy(&rec[CMPC_REC_FLAGS], &flags, 4);
   std::memcpy(&rec[CMPC_REC_TRAJ(N)], s.traj.data(), sizeof(float) * 12 * N);
   std::memcpy(&rec[CMPC_REC_GAIT(N)], s.gait.data(), 4 * N);
 
   std::vector<float> forces(12 * N);
   uint8_t st = 0;
-  if (s.use_jcqp == 1 || s.use_jcqp == 2) {
-    // use_jcqp == 1 (SolverMPC.cpp:818-838, 1057-1062): ADMM over the full QP; use_jcqp == 2
-    // (:984-1053): over the reduced one; any horizon (QPs beyond 120 variables keep M^-1 in a
-    // global slab). The reference keeps JCQP's solution whatever the residual (status 0 or 1),
-    // so no failure message for those
-    cmpc_admm_settings as{s.max_iterations, s.rho, s.sigma, s.solver_alpha, s.terminate,
-                          s.use_jcqp == 2 ? 1 : 0};
-    if (admm_host(s.h, rec.data(), N, as, forces.data(), &st) != 0) {
-      std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
-      return;
-    }
-    if (st != 0 && st != 1) {  // not solved at all: keep the previous solution, as qpOASES' failure
-      std::printf("failed to solve!\n");
-      return;
-    }
-    s.q_soln.assign(12 * N, 0.0);
-    for (int i = 0; i < 12 * N; i++) s.q_soln[i] = forces[i];
-    s.has_solved = 1;
-    return;
-  }
-  if (cmpc_batch_solve_host(s.h, rec.data(), 1, forces.data(), &st, nullptr) != 0) {
+  if (solve_single_device(s, rec.data(), N, forces.data(), &st) != 0) {
     std::fprintf(stderr, "[cmpc] %s\n", cmpc_last_error());
     return;
   }
-  if (st != CMPC_OK) std::printf("failed to solve!\n");  // SolverMPC.cpp:967
+  // SolverMPC.cpp:783, 798 (f_est itself came back with the forces)
+  for (int i = 0; i < 6; i++) f_est_smoothed[i] = 0.95f * f_est_smoothed[i] + 0.05f * f_est[i];
+  f_est_static[3] = 0.97f * f_est_static[3] + 0.03f * f_ext[3];
+  const bool admm = (s.use_jcqp == 1 || s.use_jcqp == 2);
+  // qpOASES failure: print and keep the previous solution (SolverMPC.cpp:967); the reference
+  // keeps JCQP's solution whatever its residual (status 0 or 1)
+  if (admm ? (st != 0 && st != 1) : (st != CMPC_OK)) {
+    std::printf("failed to solve!\n");
+    if (admm) return;
+  }
   s.q_soln.assign(12 * N, 0.0);
   for (int i = 0; i < 12 * N; i++) s.q_soln[i] = forces[i];
   s.has_solved = 1;

@@ -20,9 +20,8 @@
 //   * DFT peak: a 400-point Stockham FFT of the band in LDS (radices 4, 4, 5, 5; twiddles from a
 //     quarter-period table of 100 sincospi values, the other quarters by symmetry), then thread
 //     t < 100 takes |X_k|^2 of bins t+1 and t+101; the first maximum over bins 1..200 (the
-//     reference's rfft agrees to ~1e-13 relative on the magnitudes). Round 2's 200 Goertzel
-//     recurrences (400 dependent fp64 steps each) stay behind -DCMPC_EST_GOERTZEL=1: the FFT cut
-//     the launch from 1.03 to 0.75 ms at config 5;
+//     reference's rfft agrees to ~1e-13 relative on the magnitudes). It replaced round 2's 200
+//     Goertzel recurrences (400 dependent fp64 steps each): 1.03 -> 0.75 ms at config 5;
 //   * mean / std / argmax: wave butterflies plus one LDS exchange.
 // Instances outside the estimation window only push their sample (a few words of HBM traffic)
 // and evaluate the compensation.
@@ -40,12 +39,10 @@ constexpr int NFIR = W / NOUT;
 constexpr int NTAPS7 = 2 * kGaussR7 + 1, NTAPS27 = 2 * kGaussR27 + 1;
 static_assert(W % NOUT == 0 && NFIR <= NT && NBIN <= 2 * NT, "estimator thread mapping");
 
-// DFT of the band: 0 = mixed-radix Stockham FFT (radices 4, 4, 5, 5) in LDS; 1 = one Goertzel
-// recurrence per bin (the round-2 form, 200 x 400 dependent fp64 steps per instance)
-#ifndef CMPC_EST_GOERTZEL
-#define CMPC_EST_GOERTZEL 0
-#endif
+// DFT of the band: mixed-radix Stockham FFT (radices 4, 4, 5, 5) in LDS, one pass per stage:
+// thread j < W / R handles sub-transform j of a radix-R stage, so every stage needs W / 4 threads
 static_assert(W == 400, "the FFT's radix plan is 4 * 4 * 5 * 5");
+static_assert(NT >= W / 4, "fft_stage has no stride loop: one thread per radix-4 butterfly");
 constexpr int QW = W / 4;  // quarter-period twiddle table
 
 struct SharedE {
@@ -214,7 +211,7 @@ __device__ void residual(const float* __restrict__ lg, const float* __restrict__
 __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
     float* __restrict__ est, const float* __restrict__ logs, const float* __restrict__ fext3,
     const float* __restrict__ times, float sim_time, float* __restrict__ recs, int rec_words,
-    float* __restrict__ fext6, const float* __restrict__ gauss, int batch) {
+    float* __restrict__ fext6, const float* __restrict__ gauss, int batch, float* __restrict__ fest_out) {
   __shared__ SharedE sh;
   const int inst = blockIdx.x;
   if (inst >= batch) return;
@@ -256,13 +253,11 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
     for (int i = tid; i < W; i += NT) sh.fir.d[dslot(i)] = (double)st[CMPC_EST_F + (head + i) % W];
     for (int i = tid; i < NTAPS7; i += NT) sh.fir.k7[i] = (double)gauss[i];  // float taps, exact
     for (int i = tid; i < NTAPS27; i += NT) sh.fir.k27[i] = (double)gauss[NTAPS7 + i];
-#if !CMPC_EST_GOERTZEL
     if (tid < QW) {
       double sn, cs;
       sincospi(2.0 * tid / W, &sn, &cs);
       sh.tw[tid] = make_double2(cs, -sn);
     }
-#endif
     if (tid == 0) {
       sh.t0 = st[CMPC_EST_T + head];
       sh.t1 = st[CMPC_EST_T + (head + 1) % W];
@@ -287,7 +282,6 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
     const double sd = sqrt(block_sum_d(part, sh) / W);
     double v = __builtin_huge_val();
     int bi = 0x7fffffff;
-#if !CMPC_EST_GOERTZEL
     // |DFT|^2 of bins tid+1 and tid+101 from a 400-point FFT of the band (4 stages, a barrier
     // each; the reference's rfft, SolverMPC.cpp:503, agrees to ~1e-13 relative on the magnitudes)
     fft_stage<4, 1, true>(nullptr, sh.band, sh.fa, sh.tw, tid);
@@ -305,36 +299,6 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
       const double mb = xb.x * xb.x + xb.y * xb.y;
       if (mb > ma) { v = -mb; bi = kb; } else { v = -ma; bi = ka; }
     }
-#else
-    // |DFT|^2 of bins tid+1 and tid+101 by Goertzel recurrences
-    if (tid < NBIN / 2) {
-      const int ka = tid + 1, kb = tid + 1 + NBIN / 2;
-      double ca, sa, cb, sb;
-      sincospi(2.0 * ka / W, &sa, &ca);
-      sincospi(2.0 * kb / W, &sb, &cb);
-      (void)sa;
-      (void)sb;
-      const double pa = 2.0 * ca, pb = 2.0 * cb;
-      double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
-      const double2* bb = reinterpret_cast<const double2*>(sh.band);
-#pragma unroll 4
-      for (int t2 = 0; t2 < W / 2; t2++) {
-        const double2 x = bb[t2];
-        double a0 = fma(pa, a1, x.x) - a2;
-        double b0 = fma(pb, b1, x.x) - b2;
-        a2 = a1; a1 = a0;
-        b2 = b1; b1 = b0;
-        a0 = fma(pa, a1, x.y) - a2;
-        b0 = fma(pb, b1, x.y) - b2;
-        a2 = a1; a1 = a0;
-        b2 = b1; b1 = b0;
-      }
-      const double ma = a1 * a1 + a2 * a2 - pa * a1 * a2;
-      const double mb = b1 * b1 + b2 * b2 - pb * b1 * b2;
-      // the larger magnitude, ties to the smaller bin (negated for the min-reduction)
-      if (mb > ma) { v = -mb; bi = kb; } else { v = -ma; bi = ka; }
-    }
-#endif
     // first maximum: reduce on (-|X|^2, k)
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -368,6 +332,7 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
     }
     rec[CMPC_REC_FEST3] = f_est3;
     reinterpret_cast<uint32_t*>(rec)[CMPC_REC_FLAGS] = (count > CMPC_EST_STOP) ? 1u : 0u;
+    if (fest_out) fest_out[inst] = f_est3;
   }
 }
 
@@ -375,10 +340,11 @@ __global__ __launch_bounds__(NT) void cmpc_estimate_kernel(
 
 hipError_t launch_estimate(float* d_est, const float* d_logs, const float* d_fext3,
                            const float* d_time, float sim_time, float* d_records, int rec_words,
-                           float* d_fext6, const float* d_gauss, int batch, hipStream_t stream) {
+                           float* d_fext6, const float* d_gauss, int batch, hipStream_t stream,
+                           float* d_fest_out) {
   if (batch <= 0) return hipSuccess;
   hipLaunchKernelGGL(cmpc_estimate_kernel, dim3(batch), dim3(NT), 0, stream, d_est, d_logs, d_fext3,
-                     d_time, sim_time, d_records, rec_words, d_fext6, d_gauss, batch);
+                     d_time, sim_time, d_records, rec_words, d_fext6, d_gauss, batch, d_fest_out);
   return hipGetLastError();
 }
 

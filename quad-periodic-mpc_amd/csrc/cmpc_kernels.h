@@ -96,9 +96,12 @@ hipError_t launch_classg(const float* d_recs, int batch, const KParams& P, float
 constexpr int kGaussR7 = 21;   // ceil(3 * 7)
 constexpr int kGaussR27 = 81;  // ceil(3 * 27)
 constexpr int kGaussTaps = 2 * kGaussR7 + 1 + 2 * kGaussR27 + 1;
+// d_fest_out (optional): f_est(3) of instance i also to d_fest_out[i] (the single-instance ABI
+// reads it back with the forces)
 hipError_t launch_estimate(float* d_est, const float* d_logs, const float* d_fext3,
                            const float* d_time, float sim_time, float* d_records, int rec_words,
-                           float* d_fext6, const float* d_gauss, int batch, hipStream_t stream);
+                           float* d_fext6, const float* d_gauss, int batch, hipStream_t stream,
+                           float* d_fest_out = nullptr);
 // batched input assembly (cmpc_assemble.hip): one control tick per instance
 hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, uint8_t* d_due,
                            int batch, hipStream_t stream);

@@ -39,6 +39,21 @@ def trot_table(horizon: int, iteration: np.ndarray, period: int = 18) -> np.ndar
     return (prog < durations[None, None, :]).astype(np.int32).reshape(iteration.shape[0], 4 * horizon)
 
 
+def gait_table(horizon: int, iteration: np.ndarray, offsets, durations, period: int = 18) -> np.ndarray:
+    """OffsetDurationGait::getMpcTable (Gait.cpp:159-188) for any offset/duration gait: row i is
+    iteration (i + it + 1) mod P, foot j in stance iff (row - offset_j) mod P < duration_j.
+    Returns int32 [len(iteration), 4 * horizon] (step-major, foot-minor). The caller chooses P;
+    for N > P the reference would read past its P-row table."""
+    P = int(period)
+    off = np.asarray(offsets, np.int64)
+    dur = np.asarray(durations, np.int64)
+    i = np.arange(horizon)[None, :, None]
+    it = (i + np.asarray(iteration)[:, None, None] + 1) % P
+    prog = it - off[None, None, :]
+    prog = np.where(prog < 0, prog + P, prog)
+    return (prog < dur[None, None, :]).astype(np.int32).reshape(len(iteration), 4 * horizon)
+
+
 def euler_zyx_to_quat(roll, pitch, yaw):
     cr, sr = np.cos(roll / 2), np.sin(roll / 2)
     cp, sp = np.cos(pitch / 2), np.sin(pitch / 2)
@@ -120,17 +135,20 @@ def instance_draws(first_id: int, batch: int, horizon: int, seed: int = BASE_SEE
 def make_instances(batch: int, horizon: int = 10, seed: int = BASE_SEED, dt: float = 0.026,
                    random_contact_frac: float = 0.25, body_height: float = 0.29,
                    x_drag_range: float = 0.5, stress: bool = False, first_id: int = 0,
-                   chunk: int = 65536) -> np.ndarray:
+                   chunk: int = 65536, gait: str = "trotting") -> np.ndarray:
     """Return packed records [batch, record_words(horizon)] (float32) for instance ids
     ``first_id .. first_id + batch - 1``.
 
     Every instance draws from its own Philox stream (key = (seed, 0x5EED0000 + id)), so a shard
     of ids reproduces the same instances as a whole-batch call. ``stress`` widens the
-    velocity/orientation errors so friction cones bind (active sets)."""
+    velocity/orientation errors so friction cones bind (active sets). ``gait`` names one of the
+    controller's OffsetDurationGait tables (``loco_gaits``, ConvexMPCLocomotion.cpp:41-51), with
+    the period stretched to N when N > 18: "standing" puts every foot in stance at every step
+    (n = 12 N), "walking" three feet on average."""
     if batch > chunk:  # bounded temporaries for very large batches
         return np.concatenate([
             make_instances(min(chunk, batch - a), horizon, seed, dt, random_contact_frac,
-                           body_height, x_drag_range, stress, first_id + a, chunk)
+                           body_height, x_drag_range, stress, first_id + a, chunk, gait)
             for a in range(0, batch, chunk)], axis=0)
     B, N = batch, horizon
     d = instance_draws(first_id, B, N, seed)
@@ -154,11 +172,16 @@ def make_instances(batch: int, horizon: int = 10, seed: int = BASE_SEED, dt: flo
     r = np.concatenate([rx, ry, rz], axis=1)
     # contact table: trot at a random phase; a fraction with Bernoulli(0.5) contacts
     phase = np.minimum((d.uniform(_S_PHASE) * 18).astype(np.int64), 17)
-    gait = trot_table(N, phase)
+    if gait == "trotting":
+        table = trot_table(N, phase)
+    else:
+        P = max(18, N)
+        off, dur, _ = loco_gaits(P)[gait]
+        table = gait_table(N, phase % P, off, dur, P)
     rnd = d.uniform(_S_RND) < random_contact_frac
     if rnd.any():
         bern = d.uniform(_S_FIXED, count=4 * N).reshape(B, 4 * N)
-        gait[rnd] = (bern[rnd] < 0.5).astype(np.int32)
+        table[rnd] = (bern[rnd] < 0.5).astype(np.int32)
     # trajectory (ConvexMPCLocomotion.cpp:554-585)
     vdes_x = d.uniform(_S_VDX, -0.7, 0.7) * scale
     vdes_y = d.uniform(_S_VDY, -0.4, 0.4) * scale
@@ -180,7 +203,7 @@ def make_instances(batch: int, horizon: int = 10, seed: int = BASE_SEED, dt: flo
         traj[:, i, 2] = traj[:, i - 1, 2] + np.float32(dt) * traj[:, i, 8]
     x_drag = d.uniform(_S_XDRAG, -x_drag_range, x_drag_range)
     rpy = np.stack([roll, pitch, yaw], -1)
-    return pack_records(p, v, q, w, r, traj.reshape(B, 12 * N), gait, rpy=rpy, x_drag=x_drag)
+    return pack_records(p, v, q, w, r, traj.reshape(B, 12 * N), table, rpy=rpy, x_drag=x_drag)
 
 
 def make_disturbance(batch: int, steps: int, seed: int = BASE_SEED + 5, dt: float = 0.026,

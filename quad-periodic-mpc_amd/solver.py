@@ -28,6 +28,7 @@ LIB_PATH = os.environ.get("CMPC_LIB", os.path.join(PKG, "libcmpc_hip.so"))
 EXPORTED_SYMBOLS = (
     "setup_problem", "update_problem_data", "get_solution", "update_solver_settings",
     "update_problem_data_floats", "_Z13update_x_dragf", "f_ext", "simulation_time",
+    "f_est", "f_est_smoothed", "f_est_static",
     "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
     "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
     "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing", "cmpc_batch_estimate",
@@ -175,6 +176,14 @@ def set_f_ext(values) -> None:
 
 def set_simulation_time(t: float) -> None:
     ctypes.c_float.in_dll(load_library(), "simulation_time").value = float(t)
+
+
+def get_f_est(name: str = "f_est") -> np.ndarray:
+    """The solver's estimator globals (SolverMPC.h:72-74): ``f_est``, ``f_est_smoothed`` or
+    ``f_est_static`` after the last update_problem_data* call."""
+    if name not in ("f_est", "f_est_smoothed", "f_est_static"):
+        raise ValueError(name)
+    return np.array((ctypes.c_float * 6).in_dll(load_library(), name)[:], np.float32)
 
 
 # ---------------------------------------------------------------------------------------------

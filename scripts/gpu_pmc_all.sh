@@ -2,7 +2,7 @@
 # Counter passes for the bench workloads: per case, FETCH_SIZE and WRITE_SIZE in separate runs
 # (HBM bytes, MI355X_MICROARCH.md §HBM), then two SQ passes (VALU / LDS / wait mix), each its own
 # rocprofv3 --kernel-trace --pmc run with a hard time limit. Summarised by scripts/pmc_collect.py.
-# usage: scripts/gpu_pmc_all.sh <tag> [case ...]   cases: cfg3 cfg5 n16
+# usage: scripts/gpu_pmc_all.sh <tag> [case ...]   cases: cfg2 cfg3 cfg5 n16
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-pmc}
@@ -17,6 +17,7 @@ PASS_sq1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WA
 PASS_sq2="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 for c in $CASES; do
   case $c in
+    cfg2) args="--config 2" ;;
     cfg3) args="--config 3" ;;
     cfg5) args="--config 5" ;;
     n16) args="--horizon 16 --random-contact-frac 0" ;;

@@ -26,7 +26,8 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CASES = {"cfg3": dict(horizon=10, batch=65536, config=3),
+CASES = {"cfg2": dict(horizon=10, batch=4096, config=2),
+         "cfg3": dict(horizon=10, batch=65536, config=3),
          "cfg5": dict(horizon=20, batch=65536, config=5),
          "n16": dict(horizon=16, batch=65536, config=3)}
 SIMDS = 1024

@@ -65,23 +65,44 @@ def build_set(name, records, prm, cond_count=0):
     print(name, records.shape, "status", np.bincount(st), "nWSR mean", nw.mean())
 
 
-def main():
-    orc.build()
-    build_set("n10_mixed", cm.make_instances(48, 10, seed=1001), cm.make_params(10), cond_count=4)
-    build_set("n10_stress", cm.make_instances(16, 10, seed=1002, stress=True), cm.make_params(10))
-    build_set("n10_edge", edge_records(10), cm.make_params(10), cond_count=1)
-    build_set("n16_trot", cm.make_instances(8, 16, seed=1003, random_contact_frac=0.0), cm.make_params(16))
-    build_set("n19_mixed", cm.make_instances(8, 19, seed=1004), cm.make_params(19))
-    build_set("n20_trot", cm.make_instances(8, 20, seed=1005, random_contact_frac=0.0),
-              cm.make_params(20), cond_count=1)
+def gait_set(count, N, seed, gait):
+    return cm.make_instances(count, N, seed=seed, random_contact_frac=0.0, gait=gait)
+
+
+# name -> (records, params, cond_count)
+SETS = {
+    "n10_mixed": lambda: (cm.make_instances(48, 10, seed=1001), cm.make_params(10), 4),
+    "n10_stress": lambda: (cm.make_instances(16, 10, seed=1002, stress=True), cm.make_params(10), 0),
+    "n10_edge": lambda: (edge_records(10), cm.make_params(10), 1),
+    "n16_trot": lambda: (cm.make_instances(8, 16, seed=1003, random_contact_frac=0.0), cm.make_params(16), 0),
+    "n19_mixed": lambda: (cm.make_instances(8, 19, seed=1004), cm.make_params(19), 0),
+    "n20_trot": lambda: (cm.make_instances(8, 20, seed=1005, random_contact_frac=0.0), cm.make_params(20), 1),
     # general size class (n > 128): random contacts at N = 20 and all-stance at N = 12
-    build_set("n20_mixed", cm.make_instances(16, 20, seed=1006, random_contact_frac=1.0),
-              cm.make_params(20))
-    build_set("n12_allstance", allstance_records(12, 4), cm.make_params(12), cond_count=1)
+    "n20_mixed": lambda: (cm.make_instances(16, 20, seed=1006, random_contact_frac=1.0), cm.make_params(20), 0),
+    "n12_allstance": lambda: (allstance_records(12, 4), cm.make_params(12), 1),
+    # the controller's other gaits (ConvexMPCLocomotion.cpp:46, :48) at the deployed horizon
+    # N = 16 (ros_config.yaml:93) and at N = 20: standing n = 12 N (192 / 240: the 192- and
+    # 256-column classes), walking n = 138..141 at N = 16 (144 class) and 180 at N = 20 (192)
+    "n16_standing": lambda: (gait_set(8, 16, 1010, "standing"), cm.make_params(16), 1),
+    "n20_standing": lambda: (gait_set(8, 20, 1011, "standing"), cm.make_params(20), 0),
+    "n16_walking": lambda: (gait_set(8, 16, 1012, "walking"), cm.make_params(16), 0),
+    "n20_walking": lambda: (gait_set(8, 20, 1013, "walking"), cm.make_params(20), 0),
+    # class G (n > 256): standing at N = 22 (n = 264) and N = 24 (n = 288, CMPC_MAX_HORIZON)
+    "n22_standing": lambda: (gait_set(4, 22, 1014, "standing"), cm.make_params(22), 0),
+    "n24_standing": lambda: (gait_set(4, 24, 1015, "standing"), cm.make_params(24), 0),
+}
 
 
-if __name__ == "__main__" and len(sys.argv) == 1:
-    main()
+def main(names):
+    orc.build()
+    for name in names:
+        recs, prm, cond = SETS[name]()
+        build_set(name, recs, prm, cond_count=cond)
+
+
+if __name__ == "__main__" and (len(sys.argv) == 1 or sys.argv[1] != "config5"):
+    # no arguments: every set; otherwise the named ones (the others stay byte-identical)
+    main(sys.argv[1:] or list(SETS))
 
 
 def build_config5_set(name="n20_config5", batch=32, steps=520, N=20):

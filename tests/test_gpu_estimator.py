@@ -158,3 +158,44 @@ def test_config5_full_size_sampled_live_reference(cm, orc, solver_mod, on_stream
     ok = st_ref == 0
     assert ok.mean() > 0.99
     assert_parity(orc, rec_s, prm, forces.cpu().numpy()[idx], q_ref, ok, label="config 5 sampled")
+
+
+@pytest.mark.parametrize("inst", [0, 7, 21])
+def test_abi_estimator_sequence(cm, orc, inst, tmp_path):
+    """The drop-in ABI's config-5 path: 520 update_problem_data_floats calls with f_ext and
+    simulation_time set as ConvexMPCLocomotion.cpp:639-836 feeds them (in a fresh process: the
+    estimator state is process-global, as the reference's). Per call the exported f_est(3)
+    matches the oracle's est_step restatement of SolverMPC.cpp:688-798 within 1e-5, and
+    f_est_smoothed / f_est_static follow :783 / :798; the last call's forces (f_est in qg, more
+    than 500 samples) match the reference pipeline's qpOASES solve of the same record by the
+    N = 20 rule of tests/test_gpu_parity.py."""
+    import os
+    import subprocess
+    import sys
+    from test_gpu_parity import assert_parity
+    g = load_golden("n20_config5")
+    prm = golden_params(cm, g)
+    out = tmp_path / f"abi_{inst}.npz"
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "abi_estimator_child.py")
+    r = subprocess.run([sys.executable, child, str(inst), str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = np.load(out)
+    ref = g["fest_ref"][inst]
+    got = d["fest"][:, 3]
+    assert ((got == 0) == (ref == 0)).all()           # compensation starts at 400 samples
+    assert (np.abs(got - ref) / np.maximum(np.abs(ref), 1.0)).max() <= 1e-5
+    assert (d["fest"][:, [0, 1, 2, 4, 5]] == 0).all()
+    sm = np.float32(0.0)
+    st = np.float32(0.0)
+    for k in range(len(got)):
+        sm = np.float32(0.95) * sm + np.float32(0.05) * got[k]
+        st = np.float32(0.97) * st + np.float32(0.03) * np.float32(g["f3"][inst, k])
+        assert abs(d["smooth"][k, 3] - sm) <= 1e-6 * max(1.0, abs(sm))
+        assert abs(d["static"][k, 3] - st) <= 1e-6 * max(1.0, abs(st))
+    f = d["forces"].astype(np.float32)[None]
+    if orc.ref_available():
+        assert_parity(orc, g["final_records"][inst:inst + 1], prm, f, g["q_ref"][inst:inst + 1],
+                      label=f"ABI config 5 instance {inst}")
+    else:
+        assert rel_force_err(f, g["q_ref"][inst:inst + 1]).max() <= 1e-4

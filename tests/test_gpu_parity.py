@@ -5,15 +5,14 @@ reference pipeline run live on the same seeded inputs.
 Tolerance (north_star): ground-reaction forces within 1e-4 relative to qpOASES, norm-wise per
 instance: |f - f_ref|_inf / max(|f_ref|_inf, 1 N) <= 1e-4 at every horizon, N = 20 included.
 
-N <= 16 (the deployed horizon, ros_config.yaml:93) is held to that bound on every instance.
-At N >= 17 the reference's own fp32 pipeline is itself up to ~1e-4 away from the optimum of the
+Every horizon the reference admits (N <= 19, SolverMPC.cpp:113-116) is held to that bound on
+every instance. At N >= 20 (the cap lifted for config 5) the reference's own fp32 pipeline is itself up to ~1e-4 away from the optimum of the
 QP it approximates (scripts/exact_gap.py: 9.97e-5 on the live N = 20 set below, cond(H) ~ 3e3),
 so two correct fp32 implementations can differ by up to twice that. There, an instance that
-misses 1e-4 against qpOASES still passes if it is within 1e-4 of the float64 optimum of the same
-reference pipeline (oracle.fp64_solve: fp64 expm, condensation and qpOASES) — i.e. it is at least
-as accurate as north_star asks, measured against the exact answer rather than against the
-reference's rounding. Every such instance is counted, printed with its errors, and capped
-(<= 2 % of a batch).
+misses 1e-4 against qpOASES still passes if it is within 5e-5 of the float64 optimum of the same
+reference pipeline (oracle.fp64_solve: fp64 expm, condensation and qpOASES) — twice as close to
+the exact answer as north_star asks of the reference's rounding (measured round 3: <= 3.5e-5).
+Every such instance is counted, printed with its errors, and capped (<= 2 % of a batch).
 """
 import importlib
 
@@ -29,11 +28,12 @@ def tol_for(N):
     return 1e-4
 
 
-FP64_BRANCH_MIN_N = 17   # below this every instance is held to 1e-4 against qpOASES
+FP64_BRANCH_MIN_N = 20   # below this every instance is held to 1e-4 against qpOASES
+FP64_BRANCH_TOL = 5e-5   # the fallback's bound against the fp64 optimum
 
 
 def assert_parity(orc, recs, prm, f, q_ref, ok=None, label=""):
-    """err vs qpOASES <= 1e-4; at N >= 17 only, err vs the fp64 optimum <= 1e-4 instead, for at
+    """err vs qpOASES <= 1e-4; at N >= 20 only, err vs the fp64 optimum <= 5e-5 instead, for at
     most 2 % of the batch (module doc). Prints how many instances took that branch."""
     ok = np.ones(len(q_ref), bool) if ok is None else ok
     err = rel_force_err(f[ok], q_ref[ok])
@@ -50,7 +50,7 @@ def assert_parity(orc, recs, prm, f, q_ref, ok=None, label=""):
         print(msg + f" -> fp64-optimum branch: worst vs qpOASES {err[bad].max():.2e}, "
               f"worst vs fp64 optimum {max(e64s):.2e}")
         assert len(bad) <= max(1, int(0.02 * len(err))), (len(bad), err.max())
-        assert max(e64s) <= tol_for(prm.horizon), (err.max(), max(e64s))
+        assert max(e64s) <= FP64_BRANCH_TOL, (err.max(), max(e64s))
         return
     print(msg)
     assert len(bad) == 0, (err.max(), int(np.argmax(err)))
@@ -72,13 +72,18 @@ def gpu_solve(solver_mod, prm, recs):
 
 
 @pytest.mark.parametrize("name", GOLDEN_SETS)
-def test_forces_match_qpoases_golden(cm, solver_mod, name):
+def test_forces_match_qpoases_golden(cm, orc, solver_mod, name):
     g = load_golden(name)
     prm = golden_params(cm, g)
     f, st, it = gpu_solve(solver_mod, prm, g["records"])
-    assert (st == 0).all(), (name, st)
-    err = rel_force_err(f, g["q_ref"])
-    assert err.max() <= tol_for(prm.horizon), (name, err.max(), int(err.argmax()))
+    ok = g["status"] == 0
+    assert (st[ok] == 0).all(), (name, st)
+    if prm.horizon < FP64_BRANCH_MIN_N or not orc.ref_available():
+        err = rel_force_err(f[ok], g["q_ref"][ok])
+        print(f"[golden] {name}: max err vs qpOASES {err.max():.2e}")
+        assert err.max() <= tol_for(prm.horizon), (name, err.max(), int(err.argmax()))
+    else:
+        assert_parity(orc, g["records"], prm, f, g["q_ref"], ok, label=f"golden {name}")
 
 
 @pytest.mark.parametrize("name", ["n10_mixed", "n10_edge"])
@@ -112,19 +117,37 @@ def test_edge_cases(cm, solver_mod):
     assert np.all(f[swing] == 0.0)                     # swing legs exactly zero (SolverMPC.cpp:975)
 
 
-@pytest.mark.parametrize("N,stress,frac", [(10, False, 0.25), (10, True, 0.25), (10, False, 1.0),
-                                            (5, False, 0.25), (16, False, 0.0), (1, False, 0.5),
-                                            (20, False, 1.0), (12, True, 1.0)])
-def test_random_batches_match_reference_live(cm, orc, solver_mod, N, stress, frac):
+# (N, stress, random-contact fraction, gait, batch). The controller's gaits
+# (ConvexMPCLocomotion.cpp:41-51): standing puts every foot in stance (n = 12 N: the 192-column
+# class at N = 16, 256 at N = 20, class G at N = 22 / 24), walking three feet (n = 138-141 at
+# N = 16: the 144 class; 180 at N = 20: 192). N = 17..19 random contacts: the horizons the
+# reference admits beyond the deployed one, held strictly.
+LIVE_CASES = [(10, False, 0.25, "trotting", 512), (10, True, 0.25, "trotting", 512),
+              (10, False, 1.0, "trotting", 512), (5, False, 0.25, "trotting", 512),
+              (16, False, 0.0, "trotting", 512), (1, False, 0.5, "trotting", 512),
+              (20, False, 1.0, "trotting", 512), (12, True, 1.0, "trotting", 512),
+              (17, False, 1.0, "trotting", 512), (19, False, 1.0, "trotting", 512),
+              (19, True, 0.25, "trotting", 512),
+              (16, False, 0.0, "standing", 512), (20, False, 0.0, "standing", 512),
+              (16, False, 0.0, "walking", 512), (20, False, 0.0, "walking", 512),
+              (16, True, 0.0, "standing", 256),
+              (22, False, 0.0, "standing", 128), (24, False, 0.0, "standing", 128)]
+
+
+@pytest.mark.parametrize("N,stress,frac,gait,B", LIVE_CASES)
+def test_random_batches_match_reference_live(cm, orc, solver_mod, N, stress, frac, gait, B):
     if not orc.ref_available():
         pytest.skip("oracle/_ref not present")
     prm = cm.make_params(N)
-    recs = cm.make_instances(512, N, seed=7000 + N, stress=stress, random_contact_frac=frac)
+    recs = cm.make_instances(B, N, seed=7000 + N, stress=stress, random_contact_frac=frac, gait=gait)
     q, st_ref, _ = orc.ref_solve_batch(recs, prm, nthreads=16)
     f, st, it = gpu_solve(solver_mod, prm, recs)
     ok = st_ref == 0
-    assert (st[ok] == 0).all()
-    assert_parity(orc, recs, prm, f, q, ok, label=f"live stress={stress} frac={frac}")
+    n = 3 * (cm.unpack_gait(recs, N) != 0).sum(1)
+    print(f"[live] N={N} {gait} stress={stress} frac={frac}: n {n.min()}..{n.max()}, "
+          f"qpOASES solved {ok.sum()} of {B}")
+    assert (st[ok] == 0).all(), np.bincount(st[ok])
+    assert_parity(orc, recs, prm, f, q, ok, label=f"live {gait} stress={stress} frac={frac}")
 
 
 CLASS_EDGES = [0, 60, 64, 80, 96, 120, 128, 144, 192, 256]  # class 1 (60 / 64 builds), wide 80 .. 256
@@ -219,7 +242,8 @@ def test_reference_call_protocol(cm, orc, solver_mod):
 def test_single_instance_fast_path_bitwise(cm, solver_mod, N, frac):
     """batch == 1 from host memory takes the one-kernel fast path (host-counted size class, no
     classify pass); it must reproduce the batched launch bit for bit, in every size class
-    (N = 10 with random contacts: class 1 and wide 80/96; N = 20: wide 128/192/256)."""
+    (N = 10 with random contacts: class 1 (64-wide build) and wide 80 / 96; N = 20 random
+    contacts: wide 120 / 128 / 144 / 192)."""
     prm = cm.make_params(N)
     recs = cm.make_instances(48, N, seed=900 + N, random_contact_frac=frac)
     f_b, st_b, it_b = gpu_solve(solver_mod, prm, recs)
@@ -231,3 +255,45 @@ def test_single_instance_fast_path_bitwise(cm, solver_mod, N, frac):
             np.testing.assert_array_equal(f1[0], f_b[i])
     finally:
         s.close()
+
+
+@pytest.mark.parametrize("N", [10, 16, 20])
+def test_batch_size_invariance(cm, solver_mod, N):
+    """The same record gets the same forces whatever batch it is solved in. The launch
+    sequence depends on the batch size (cmpc_launch.hip: class 1 as one 64-wide build below
+    16384 instances and as 60- plus 64-wide builds from there; the wide classes one workgroup per
+    entry or persistent), so one 16384-instance random-contact batch (every size class) is solved
+    whole, in four pieces of 4096, and, for a sample across the classes, one instance at a time
+    (the single-instance fast path); forces, status and iteration counts must agree bit for
+    bit."""
+    prm = cm.make_params(N)
+    B = 16384
+    recs = cm.make_instances(B, N, seed=8300 + N, random_contact_frac=1.0)
+    f_all, st_all, it_all = gpu_solve(solver_mod, prm, recs)
+    s = solver_mod.BatchSolver(prm, max_batch=4096)
+    try:
+        parts = [s.solve_host(recs[a:a + 4096]) for a in range(0, B, 4096)]
+    finally:
+        s.close()
+    f_p = np.concatenate([p[0] for p in parts])
+    st_p = np.concatenate([p[1] for p in parts])
+    it_p = np.concatenate([p[2] for p in parts])
+    n = 3 * (cm.unpack_gait(recs, N) != 0).sum(1)
+    diff = np.nonzero((f_p != f_all).any(1) | (st_p != st_all) | (it_p != it_all))[0]
+    if diff.size:
+        print(f"[batch-size] N={N}: {diff.size} of {B} differ; their n: {np.unique(n[diff])}")
+    assert diff.size == 0
+    rng = np.random.default_rng(N)
+    pick = []
+    for lo, hi in zip(CLASS_EDGES[:-1], CLASS_EDGES[1:]):
+        idx = np.nonzero((n > lo) & (n <= hi))[0]
+        if idx.size:
+            pick.append(rng.choice(idx, min(6, idx.size), replace=False))
+    s1 = solver_mod.BatchSolver(prm, max_batch=1)
+    try:
+        for i in np.concatenate(pick):
+            f1, st1, it1 = s1.solve_host(recs[i:i + 1])
+            assert st1[0] == st_all[i] and it1[0] == it_all[i], (i, n[i])
+            np.testing.assert_array_equal(f1[0], f_all[i], err_msg=f"instance {i}, n = {n[i]}")
+    finally:
+        s1.close()
