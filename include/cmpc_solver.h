@@ -49,7 +49,8 @@
 #define CMPC_REC_GAIT(N)   (CMPC_REC_HDR + 12 * (N))
 #define CMPC_REC_WORDS(N)  ((CMPC_REC_HDR + 13 * (N) + 3) & ~3)
 
-#define CMPC_MAX_HORIZON  24  /* reference caps at 19 (SolverMPC.cpp:113-116); lifted for N=20 */
+#define CMPC_MAX_HORIZON  20  /* reference caps at 19 (SolverMPC.cpp:113-116); lifted to 20 for config 5;
+                                 longer horizons are rejected (cmpc_batch_create / set_params -2) */
 
 /* ------------------------------------------------------------------------------------------ */
 /* Config 5: periodic-disturbance estimation (fp32 words).                                    */

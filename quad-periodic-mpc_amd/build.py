@@ -20,12 +20,19 @@ OBJ = os.path.join(ROOT, "build", "obj")
 # one translation unit per kernel family so the large unrolled kernels compile in parallel
 SOURCES = ["cmpc_wide_w256.hip", "cmpc_wide_w192.hip", "cmpc_class1.hip", "cmpc_wide_w80.hip", "cmpc_wide_w96.hip",
            "cmpc_wide_w120.hip", "cmpc_wide_w128.hip", "cmpc_wide_w144.hip", "cmpc_wide_w80p.hip",
-           "cmpc_wide_w96p.hip", "cmpc_wide_w120p.hip", "cmpc_wide_w128p.hip", "cmpc_classg.hip", "cmpc_launch.hip", "cmpc_estimator.hip", "cmpc_assemble.hip",
+           "cmpc_wide_w96p.hip", "cmpc_wide_w120p.hip", "cmpc_wide_w128p.hip", "cmpc_wide_w80r.hip",
+           "cmpc_wide_w96r.hip", "cmpc_wide_w120r.hip", "cmpc_wide_w80pr.hip", "cmpc_wide_w96pr.hip",
+           "cmpc_wide_w120pr.hip", "cmpc_condense.hip", "cmpc_launch.hip", "cmpc_estimator.hip", "cmpc_assemble.hip",
            "cmpc_admm.hip", "cmpc_quadprog.hip", "cmpc_abi.cpp"]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: the SLP pass packs adjacent row updates into v_pk_fma_f32, which ties
 # slot registers into 64-bit pairs and made the register-resident rows spill
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", "-fno-slp-vectorize"]
+# -ffp-contract=on: multiply-adds fuse only inside one source expression (clang's front end emits
+# llvm.fmuladd), never across statements in the back end, so a kernel body rounds the same in
+# every launch form it is inlined into (the one-per-entry and persistent wide builds, the
+# single-instance path); with `fast` the back end fused differently per form and the same record
+# could get different forces in batches of different sizes
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", "-fno-slp-vectorize", "-ffp-contract=on"]
 
 
 def _deps(path: str, seen=None) -> set:

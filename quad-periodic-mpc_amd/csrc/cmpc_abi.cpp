@@ -35,9 +35,7 @@ struct cmpc_batch {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int* d_work = nullptr;
-  float* d_gscratch = nullptr;   // slabs of the general size class (cmpc_classg.hip)
   float* d_gauss = nullptr;      // gaussian_filter kernels of the config-5 estimator
-  size_t gscratch_floats = 0;
   double* d_admm_slabs = nullptr;  // ADMM inverses of QPs with n > 120 (cmpc_admm.hip)
   size_t admm_slab_doubles = 0;
   int admm_nslabs = 0;
@@ -71,6 +69,12 @@ static cmpc::KParams make_kparams(const cmpc_params& p) {
   k.N = p.horizon;
   k.rec_words = CMPC_REC_WORDS(p.horizon);
   k.max_iter = p.max_iter > 0 ? p.max_iter : 100;
+  // the fp32 pipelines of the reference and of this solver are within ~1e-5 of the exact optimum
+  // at N <= 10 and drift to ~1e-4 beyond: the refinement runs from N = 11
+  k.refine = p.horizon > 10 ? 1 : 0;
+  k.dt64 = (double)k.dt;
+  k.dth64 = 0.5 * k.dt64 * k.dt64;
+  k.dt3_64 = k.dt64 * k.dt64 * k.dt64 / 6.0;
   return k;
 }
 
@@ -92,20 +96,6 @@ extern "C" const char* cmpc_last_error(void) { return g_last_error.c_str(); }
 namespace cmpc {
 void set_last_error(const char* msg) { g_last_error = msg; }  // for the other translation units
 }  // namespace cmpc
-
-// the general class needs 2 (12N)^2 floats per workgroup of its persistent grid
-static int ensure_gscratch(cmpc_batch* h) {
-  if (h->max_batch <= 0) return 0;
-  const size_t need = cmpc::classg_scratch_floats(h->prm.horizon, cmpc::classg_grid(h->max_batch));
-  if (need <= h->gscratch_floats) return 0;
-  if (h->d_gscratch) (void)hipFree(h->d_gscratch);
-  h->d_gscratch = nullptr;
-  h->gscratch_floats = 0;
-  hipError_t e = hipMalloc(&h->d_gscratch, need * sizeof(float));
-  if (e != hipSuccess) return fail("hipMalloc(class G scratch)", e);
-  h->gscratch_floats = need;
-  return 0;
-}
 
 // the ADMM kernel keeps M^-1 of QPs with more than 120 variables in per-workgroup fp64 slabs:
 // min(max_batch, kAdmmSlabs) of (12N)^2 doubles (151 MB at N = 16, 236 MB at N = 20). They are
@@ -136,7 +126,6 @@ extern "C" int cmpc_batch_set_params(cmpc_batch* h, const cmpc_params* prm) {
   }
   h->prm = *prm;
   h->kp = make_kparams(*prm);
-  if (int r = ensure_gscratch(h)) return r;
   return ensure_admm_slabs(h);
 }
 
@@ -180,7 +169,6 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
     if (e == hipSuccess) e = hipMemcpy(h->d_gauss, taps, sizeof(taps), hipMemcpyHostToDevice);
     if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("gauss taps", e); }
   }
-  if (int r = ensure_gscratch(h); r != 0) { cmpc_batch_destroy(h); return r; }
   *out = h;
   return 0;
 }
@@ -190,7 +178,6 @@ static void free_staging(cmpc_batch* h);
 extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (!h) return;
   if (h->d_work) (void)hipFree(h->d_work);
-  if (h->d_gscratch) (void)hipFree(h->d_gscratch);
   if (h->d_gauss) (void)hipFree(h->d_gauss);
   if (h->d_admm_slabs) (void)hipFree(h->d_admm_slabs);
   free_staging(h);
@@ -217,7 +204,7 @@ extern "C" int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int batch
   hipEvent_t* ev = nullptr;
   if (h->ev_steps > 0 && h->ev_next < h->ev_steps) ev = &h->ev[3 * h->ev_next++];
   hipError_t e = cmpc::launch_solve(d_records, batch, h->kp, d_forces, d_status, d_iters, h->d_work,
-                                    h->max_batch, h->d_gscratch, h->stream, h->ctx, ev);
+                                    h->max_batch, h->stream, h->ctx, ev);
   if (e != hipSuccess) return fail("launch_solve", e);
   return 0;
 }
@@ -304,8 +291,7 @@ extern "C" int cmpc_batch_read_timing(cmpc_batch* h, float* ms, int* steps_recor
 extern "C" int cmpc_batch_condense(cmpc_batch* h, const float* d_records, int batch, float* d_H,
                                    float* d_g) {
   if (!h || batch < 0 || batch > h->max_batch) return -1;
-  hipError_t e = cmpc::launch_condense(d_records, batch, h->kp, d_H, d_g, h->d_gscratch,
-                                       cmpc::classg_grid(h->max_batch), h->stream);
+  hipError_t e = cmpc::launch_condense(d_records, batch, h->kp, d_H, d_g, h->stream);
   if (e != hipSuccess) return fail("launch_condense", e);
   return 0;
 }
@@ -398,8 +384,8 @@ static int solve_single_host(cmpc_batch* h, const float* record, float* forces, 
   hipError_t e;
   if ((e = hipMemcpyAsync(h->d_rec, pin_rec, rw * sizeof(float), hipMemcpyHostToDevice, h->stream)) != hipSuccess)
     return fail("H2D", e);
-  if ((e = cmpc::launch_single(h->d_rec, n, h->kp, d_out, d_st, h->d_iters, h->d_one, h->d_gscratch,
-                               h->stream)) != hipSuccess)
+  if ((e = cmpc::launch_single(h->d_rec, n, h->kp, d_out, d_st, h->d_iters, h->d_one, h->stream)) !=
+      hipSuccess)
     return fail("launch_single", e);
   if ((e = hipMemcpyAsync(pin_out, d_out, (12 * N + 1) * sizeof(float), hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
     return fail("D2H", e);
@@ -419,9 +405,8 @@ extern "C" int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int ba
   const int N = h->prm.horizon;
   const size_t rw = (size_t)CMPC_REC_WORDS(N);
   // one instance (the reference ABI's operating mode): the fast path, unless per-launch timing
-  // is on (it brackets the batched launch sequence) or the instance needs class G's slabs
-  if (batch == 1 && h->ev_steps == 0 && host_reduced_size(records, N, h->prm.f_max) <= 256)
-    return solve_single_host(h, records, forces, status, iters);
+  // is on (it brackets the batched launch sequence)
+  if (batch == 1 && h->ev_steps == 0) return solve_single_host(h, records, forces, status, iters);
   hipError_t e;
   if ((e = hipMemcpyAsync(h->d_rec, records, rw * batch * sizeof(float), hipMemcpyHostToDevice, h->stream)) != hipSuccess)
     return fail("H2D", e);
@@ -545,13 +530,8 @@ int solve_single_device(SingleState& s, const float* rec, int N, float* forces, 
     return 0;
   }
   const int n = host_reduced_size(rec, N, h->prm.f_max);
-  if (n <= 256) {
-    e = cmpc::launch_single(h->d_rec, n, h->kp, d_out, d_st, h->d_iters, h->d_one, h->d_gscratch, h->stream);
-  } else {  // class G: its slabs and list through the batched launch sequence
-    if (int r = cmpc_batch_solve(h, h->d_rec, 1, d_out, d_st, nullptr)) return r;
-    e = hipSuccess;
-  }
-  if (e != hipSuccess) return fail("launch_single", e);
+  if ((e = cmpc::launch_single(h->d_rec, n, h->kp, d_out, d_st, h->d_iters, h->d_one, h->stream)) != hipSuccess)
+    return fail("launch_single", e);
   if ((e = hipMemcpyAsync(pin_out, d_out, (12 * N + 2) * sizeof(float), hipMemcpyDeviceToHost, h->stream)) !=
       hipSuccess)
     return fail("D2H", e);

@@ -362,19 +362,24 @@ __device__ __forceinline__ void make_bdt(const float* __restrict__ rec, const Mo
   }
 }
 
+// rpy of the record's quaternion as the reference's quat_to_rpy (SolverMPC.cpp:352-361), fp32
+__device__ __forceinline__ void quat_to_rpy(const float* __restrict__ rec, float* rpy) {
+  const float qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],
+              qz = rec[CMPC_REC_Q + 3];
+  float as = -2.f * (qx * qz - qw * qy);
+  as = fminf(as, 0.99999f);  // only the upper clamp, as the reference
+  rpy[0] = atan2f(2.f * (qy * qz + qw * qx), qw * qw - qx * qx - qy * qy + qz * qz);
+  rpy[1] = asinf(as);
+  rpy[2] = atan2f(2.f * (qx * qy + qw * qz), qw * qw + qx * qx - qy * qy - qz * qz);
+}
+
 // e_i = Adt^{i+1} x0 + sum_{k<=i} Adt^k Qdt f - X_d,i for step i (SolverMPC.cpp:592, 633-642,
 // 808-814). x0 = [rpy, p, w, v, -9.8] with rpy from quat_to_rpy (SolverMPC.cpp:352-361).
 __device__ __forceinline__ void state_error(const float* __restrict__ rec, const Model& md, int i,
                                             const float* traj_i, float* e) {
-  const float qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],
-              qz = rec[CMPC_REC_Q + 3];
   float x0[13];
   {
-    float as = -2.f * (qx * qz - qw * qy);
-    as = fminf(as, 0.99999f);  // only the upper clamp, as the reference
-    x0[0] = atan2f(2.f * (qy * qz + qw * qx), qw * qw - qx * qx - qy * qy + qz * qz);
-    x0[1] = asinf(as);
-    x0[2] = atan2f(2.f * (qx * qy + qw * qz), qw * qw + qx * qx - qy * qy - qz * qz);
+    quat_to_rpy(rec, x0);
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       x0[3 + k] = rec[CMPC_REC_P + k];
@@ -408,6 +413,14 @@ __device__ __forceinline__ void state_error(const float* __restrict__ rec, const
     if (j < 12) ev -= traj_i[j];
     e[j] = ev;
   }
+}
+
+// v_readlane of a double (lane uniform)
+__device__ __forceinline__ double rl_d(double x, int lane) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
 // Friction-pyramid constraint c = 6 s + t of stance foot-step s (reduced vars 3s, 3s+1, 3s+2):

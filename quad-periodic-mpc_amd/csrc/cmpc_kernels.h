@@ -17,7 +17,9 @@ struct KParams {
   int N;
   int rec_words;
   int max_iter;    // active-set cap; the kernels allow max_iter + 2 n
-  int pad;
+  int refine;      // wide classes: one fp64 refinement step of the converged active set (N > 10)
+  // the step's fp64 powers for that refinement (scalar registers, not per-lane conversions)
+  double dt64, dth64, dt3_64;  // dt, dt^2 / 2, dt^3 / 6
 };
 
 // Kernel-side copy of cmpc_loco_params + the handle's horizon / record stride.
@@ -31,9 +33,9 @@ struct LocoParams {
 };
 
 // Scratch ints needed by launch_solve for max_batch instances.
-// d_work: [0] instances with n > 64, [1..6] lengths of the class lists (wide classes of 80, 96,
-// 128, 192, 256 columns, general), [8 ..) the six lists of max_batch entries each
-// instance lists of the classify pass: 80, 96, 128, 192, 256, G, 144, and 7: class-1 instances
+// d_work: [0] instances with n > 64, [1 + list] lengths of the class lists, then the lists of
+// max_batch entries each. Instance lists of the classify pass: 80, 96, 128, 192, 256, (5: unused
+// since the general class went with CMPC_MAX_HORIZON = 20), 144, and 7: class-1 instances
 // with 60 < n <= 64 (the 64-wide class-1 build; n <= 60 runs in the 60-wide build over the
 // whole batch); 8: the 120-column wide build (97 <= n <= 120; the 128 build keeps 121..128).
 // d_work = [kHdr ints: cnt[0] total, cnt[1 + list] list lengths, cnt[kDeq + list] the persistent
@@ -53,17 +55,12 @@ struct LaunchCtx {
   hipEvent_t classified = nullptr;  // the classify pass (on side 0) is done
   hipEvent_t join[kSideStreams] = {nullptr, nullptr};
 };
-// Workgroups of the general class (persistent over its overflow list) and its global slabs.
-inline int classg_grid(int max_batch) { return max_batch < 2048 ? max_batch : 2048; }
-size_t classg_scratch_floats(int horizon, int grid);
-
 // ev (optional): 3 events recorded on `stream`: ev[0] before class 1, ev[1] after it, ev[2]
 // after the wider classes (side streams) have joined.
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
-                        float* d_gscratch, hipStream_t stream, const LaunchCtx& ctx,
-                        hipEvent_t* ev = nullptr);
-// per-class launchers (cmpc_class1.hip, cmpc_wide_w*.hip, cmpc_classg.hip)
+                        hipStream_t stream, const LaunchCtx& ctx, hipEvent_t* ev = nullptr);
+// per-class launchers (cmpc_class1.hip, cmpc_wide_w*.hip)
 hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream);
@@ -85,11 +82,7 @@ CMPC_DECL_WIDE(192)
 CMPC_DECL_WIDE(256)
 #undef CMPC_DECL_WIDE
 hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_forces,
-                         uint8_t* d_status, int32_t* d_iters, const int* d_one, float* d_gscratch,
-                         hipStream_t stream);
-hipError_t launch_classg(const float* d_recs, int batch, const KParams& P, float* d_forces,
-                         uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
-                         float* scratch, int grid, hipStream_t stream);
+                         uint8_t* d_status, int32_t* d_iters, const int* d_one, hipStream_t stream);
 // config 5 estimator (cmpc_estimator.hip). d_gauss: the two normalised float Gaussian kernels
 // of gaussian_filter (sigma 7: 43 taps, then sigma 27: 163 taps), built on the host exactly as
 // SolverMPC.cpp:404-418 builds them.
@@ -109,9 +102,10 @@ hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, u
 hipError_t launch_rollout(float* d_loco, const float* d_recs, const float* d_forces,
                           const float* d_xi6, const uint8_t* d_due, const LocoParams& lp, float dt,
                           int batch, hipStream_t stream);
-// parity hook: full (nothing eliminated) qH [12N x 12N] / qg [12N] per instance
+// parity hook and JCQP condensation: full (nothing eliminated) qH [12N x 12N] / qg [12N] per
+// instance (cmpc_condense.hip)
 hipError_t launch_condense(const float* d_recs, int batch, const KParams& P, float* d_H, float* d_g,
-                           float* scratch, int grid, hipStream_t stream);
+                           hipStream_t stream);
 
 // use_jcqp == 1 / 2: batched JCQP ADMM over the full / reduced condensed QP (cmpc_admm.hip).
 // Instances whose QP has n > 120 variables run on nslabs persistent workgroups with M in

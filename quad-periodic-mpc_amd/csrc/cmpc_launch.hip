@@ -2,8 +2,8 @@
 //   classify (this file): n = 3 x stance foot-steps per instance (SolverMPC.cpp:869-894), the
 //     instances with n > 64 appended to the list of their class;
 //   class 1 (cmpc_class1.hip): every instance, one wavefront each; exits when n > 64;
-//   wide classes (cmpc_wide.h: two lanes per row, NV/32 wavefronts; NV = 80, 96, 128, 192, 256)
-//     and class G (cmpc_classg.hip, any n, global slabs) each over its own list, on two side
+//   wide classes (cmpc_wide.h: two lanes per row, NV/32 wavefronts; NV = 80, 96, 120, 128, 144,
+//     192, 256; n <= 12 N <= 240 at CMPC_MAX_HORIZON = 20) each over its own list, on two side
 //     streams forked after classify, so they run concurrently with class 1 and with each
 //     other. At N = 10 they are a latency-bound tail (few, long solves); at N = 16..20 the 128-
 //     and 192-column classes carry the batch and run side by side on the two streams.
@@ -41,7 +41,7 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
     }
     const int n = 3 * nfs;
     cls = (n <= c1_max) ? -1 : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 120) ? 8
-        : (n <= 128) ? 2 : (n <= 144) ? 6 : (n <= 192) ? 3 : (n <= 256) ? 4 : 5;
+        : (n <= 128) ? 2 : (n <= 144) ? 6 : (n <= 192) ? 3 : 4;
   }
   const unsigned long long any = __ballot(cls >= 0);
   if (any == 0ull) return;
@@ -82,8 +82,7 @@ bool one_per_entry(int lo, int hi, int N, int batch) {
 
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
-                        float* d_gscratch, hipStream_t stream, const LaunchCtx& ctx,
-                        hipEvent_t* ev) {
+                        hipStream_t stream, const LaunchCtx& ctx, hipEvent_t* ev) {
   int* cnt = d_work;
   int* list[kLists];
   for (int j = 0; j < kLists; j++) list[j] = d_work + kHdr + (size_t)j * max_batch;
@@ -152,7 +151,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if (split60 && (e = launch_class1(64, d_recs, batch, P, d_forces, d_status, d_iters, list[7],
                                       &cnt[8], nullptr, nullptr, grid_of[7], ctx.side[1])) != hipSuccess)
       return e;
-    // side 0: 80, 120, 144, 256; side 1: 96, 128, 192, G (at N = 20 the 120-column class, which
+    // side 0: 80, 120, 144, 256; side 1: 96, 128, 192 (at N = 20 the 120-column class, which
     // carries the batch, runs beside the 128-column class)
     if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], dq(0, 65, 80), grid_of[0],
                              ctx.side[0])) != hipSuccess)
@@ -186,11 +185,6 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if (n_max > 192 && (e = launch_wide_w256(d_recs, P, d_forces, d_status, d_iters, list[4], &cnt[5], &cnt[kDeq + 4],
                                              grid_of[4], ctx.side[0])) != hipSuccess)
       return e;
-    const bool g_possible = n_max > 256;
-    if (g_possible && (e = launch_classg(d_recs, batch, P, d_forces, d_status, d_iters, list[5],
-                                         &cnt[6], d_gscratch, classg_grid(max_batch),
-                                         ctx.side[1])) != hipSuccess)
-      return e;
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
   // class 1 over the whole batch (it skips instances with n > its row width)
@@ -212,8 +206,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
 // record's gait table, the same test as the classify pass): exactly one kernel of the right
 // class, no classify pass, no side-stream fork/join. d_one = {1, 0}: a one-entry instance list.
 hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_forces,
-                         uint8_t* d_status, int32_t* d_iters, const int* d_one, float* d_gscratch,
-                         hipStream_t stream) {
+                         uint8_t* d_status, int32_t* d_iters, const int* d_one, hipStream_t stream) {
   const int* cnt = d_one;
   const int* lst = d_one + 1;
   if (n <= 64)
@@ -234,8 +227,7 @@ hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_f
 #undef CMPC_SINGLE_WIDE
   if (n <= 144) return launch_wide_w144(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
   if (n <= 192) return launch_wide_w192(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
-  if (n <= 256) return launch_wide_w256(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
-  return launch_classg(d_rec, 1, P, d_forces, d_status, d_iters, lst, cnt, d_gscratch, 1, stream);
+  return launch_wide_w256(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
 }
 
 }  // namespace cmpc

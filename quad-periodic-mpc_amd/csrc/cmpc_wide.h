@@ -50,6 +50,10 @@
 #ifndef CMPC_WIDE_VGPR_CAP
 #define CMPC_WIDE_VGPR_CAP 0
 #endif
+// one mixed-precision refinement step of the converged active set (wide_refine below); 0: off
+#ifndef CMPC_WIDE_REFINE
+#define CMPC_WIDE_REFINE 1
+#endif
 
 namespace cmpc {
 namespace {
@@ -100,6 +104,10 @@ struct WGeo {
   static constexpr int QI = (NV == 80) ? 56 : (NV == 96) ? 40 : (NV == 120) ? 48 : (NV == 128) ? 32 : 64;
   static constexpr int O_RINV = (GI_END + 3) & ~3;
   static constexpr int PTOT = (mx(mx(PSZ + 12 * 16, PSZ + CH), O_RINV + QI * (QI + 1) / 2) + 3) & ~3;
+  // the refinement's fp64 scratch (refine_gradient_seq: 18 + 12 N doubles) in the R^-1 area,
+  // which the active set no longer reads once it has converged
+  static_assert(2 * (24 + 12 * MAXN) <= QI * (QI + 1) / 2, "refinement scratch must fit the R^-1 area");
+  static_assert(12 * MAXN <= 2 * NT && 6 * MAXN <= NT && 3 * MAXN <= NT - 20, "refinement phases: threads per step");
   static_assert(PSZ % 4 == 0 && PSZ_R % 4 == 0 && VL % 4 == 0, "16-B aligned stage buffers");
 };
 
@@ -215,6 +223,312 @@ __device__ __forceinline__ int rli_pos(const int (&a)[RQ], int i) {
   (void)lane;                                        \
   (void)h;                                           \
   (void)r
+
+// Mixed-precision refinement of the converged active set, one step. With the working set W of the
+// dual active set, x minimises the fp32-condensed QP on the face {C_W x = b_W}; the minimiser of
+// the exact QP on that face is x - J2 J2' r, where r = H x + g is the exact QP's gradient at x and
+// J2 the columns of J past the q active positions (Goldfarb-Idnani: J2 J2' = Z (Z' H Z)^-1 Z',
+// Z spanning the null space of C_W; C_W J2 = 0, so the step keeps the active constraints). r is
+// evaluated in fp64 without H or g (SolverMPC.cpp:806-814):
+//   r = H x + g = 2 B_qp' S (A_qp x0 + B_qp x + Q_qp f - X_d) + 2 alpha x,
+// by one forward simulation of the discretised model driven by the forces x and one backward
+// (adjoint) recursion. A_c^3 = 0, so Adt = I + dt A + dt^2/2 A^2 and Bdt = (dt I + dt^2/2 A +
+// dt^3/6 A^2) B_c act as a few sparse operations (ct_ss_mats, SolverMPC.cpp:260-279: A[0:3][6:9]
+// = R', A[3:6][9:12] = I, A(11,9) = x_drag, A(11,12) = 1; B[6:9][3b..] = I_w^-1 [r_b]x, B[9:12]
+// [3b..] = I / m). The forward pass runs on the deviations z_k+1 = x_k+1 - X_d,k (= e_k, the
+// tracking error the cost weighs):
+//   z_k+1 = Adt z_k + d_k,  d_k = Bdt u_k + Qdt f + Adt X_d,k-1 - X_d,k  (X_d,-1 = x0, z_0 = 0),
+// the backward pass on mu_k = S e_k + Adt' mu_k+1, and the gradient entry of force (k, 3 b + a) is
+//   2 ((y_k x r_b)_a + nu_k[9 + a] / m) + 2 alpha x,  nu_k = (dt I + dt^2/2 A' + dt^3/6 A'^2) mu_k,
+//   y_k = I_w^-1 nu_k[6:9]  (B_c' nu_k; I_w^-1 symmetric).
+// Phases (fp64 scratch in the R^-1 area, 18 + 12 N doubles: R, I_w^-1, then 12 per step):
+//   A  thread (k, a), a < 3: t_a = sum_b (r_b x u_b)_a and s_a = sum_b u_b,a of step k;
+//   B  thread (k, j), j < 12: d_k,j (w = B_c u_k from t, s);
+//   C  wave 0, lane j < 12 owns component j: the two recursions, the cross terms by v_readlane;
+//   D  thread (k, i), i < 6: y_k (i < 3) and nu_k[9 + i - 3] / m;
+//   E  row r: its gradient entry, then u = J2' r (the columns of J summed over the rows, by DPP
+//      within a wave and over the waves in order through the LDS: deterministic) and x -= J2 u.
+// The reference's own fp32 pipeline (dense-S GEMMs) is up to ~1e-4 from its QP's exact optimum at
+// N >= 16; after this step the solution lands within ~1e-6 of it.
+template <int NV>
+__device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, const KParams& P, SharedW<NV>& sh,
+                                            float (&slot)[WGeo<NV>::NH], float& xv, int q, int n, int wave) {
+  using G = WGeo<NV>;
+  constexpr int NH = G::NH;
+  constexpr int NC = (NH + 63) / 64;
+  constexpr int S0 = 24;  // [0..8] R, [9..17] I_w^-1, [18] x_drag, [19] f_est term, [20] x0[12], [21..23] rpy
+  // This runs inside the active-set loop: an opaque record pointer keeps its loads (and the
+  // arithmetic on them) from being hoisted out of the loop and kept live across every trip. The
+  // fp64 scalars come from the kernel arguments (SGPRs) or the LDS, never long-lived VGPRs: the
+  // 96-column class has 48 VGPRs beside its J row.
+  const float* rec = rec_in;
+  asm volatile("" : "+s"(rec));
+  double* scr = reinterpret_cast<double*>(&sh.P[G::O_RINV]);
+  const int N = P.N;
+  const double dt = P.dt64, dth = P.dth64, dt3 = P.dt3_64;
+  const float* xs = sh.xs();
+  // ---- A: per step and axis, sum_b r_b x u_b and sum_b u_b; R, I_w^-1 and the instance scalars
+  {
+    const int t = 64 * wave + lane_opq();
+    if (t < 3 * N) {
+      const int k = t / 3, a = t - 3 * (t / 3);
+      const int a1 = (a == 2) ? 0 : a + 1, a2 = (a == 0) ? 2 : a - 1;
+      double tc = 0.0, sc = 0.0;
+      int v = sh.blkbase[k];
+#pragma unroll
+      for (int f = 0; f < 4; f++) {
+        if (sh.stance[4 * k + f]) {
+          // (r x u)_a = r_a1 u_a2 - r_a2 u_a1
+          tc += (double)rec[CMPC_REC_R + 4 * a1 + f] * (double)xs[v + a2] -
+                (double)rec[CMPC_REC_R + 4 * a2 + f] * (double)xs[v + a1];
+          sc += (double)xs[v + a];
+          v += 3;
+        }
+      }
+      scr[S0 + 12 * k + a] = tc;
+      scr[S0 + 12 * k + 3 + a] = sc;
+    } else if (t >= G::NT - 18) {
+      // R (Eigen toRotationMatrix, RobotState.cpp:36) entry i, or I_w^-1 = R diag(1/I_body) R'
+      // entry i - 9 (I_body: RobotState.h:25), in fp64 from the fp32 quaternion
+      const int e = t - (G::NT - 18);
+      const double qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],
+                   qz = rec[CMPC_REC_Q + 3];
+      auto rot = [&](int i, int j) -> double {
+        const double vi = (i == 0) ? qx : (i == 1) ? qy : qz;
+        const double vj = (j == 0) ? qx : (j == 1) ? qy : qz;
+        if (i == j) {
+          const double o1 = (i == 0) ? qy : qx, o2 = (i == 2) ? qy : qz;
+          return 1.0 - 2.0 * (o1 * o1 + o2 * o2);
+        }
+        const int k = 3 - i - j;
+        const double vk = (k == 0) ? qx : (k == 1) ? qy : qz;
+        const double sg = ((j - i + 3) % 3 == 1) ? 1.0 : -1.0;  // epsilon_ijk
+        return 2.0 * (vi * vj - sg * qw * vk);
+      };
+      double val;
+      if (e < 9) {
+        val = rot(e / 3, e - 3 * (e / 3));
+      } else {
+        const int i = (e - 9) / 3, j = (e - 9) - 3 * ((e - 9) / 3);
+        val = rot(i, 0) * (1.0 / 0.07) * rot(j, 0) + rot(i, 1) * (1.0 / 0.26) * rot(j, 1) +
+              rot(i, 2) * (1.0 / 0.242) * rot(j, 2);
+      }
+      scr[e] = val;
+    } else if (t == G::NT - 19) {
+      const uint32_t flags = __float_as_uint(rec[CMPC_REC_FLAGS]);
+      scr[18] = (double)rec[CMPC_REC_XDRAG];
+      scr[19] = (flags & 1u) ? (double)rec[CMPC_REC_FEST3] : 0.0;  // Q_qp f (SolverMPC.cpp:808-811)
+      scr[20] = (double)(-9.8f);
+    } else if (t == G::NT - 20) {
+      float rpy[3];  // x0's rpy as the fp32 solve computes it (quat_to_rpy)
+      quat_to_rpy(rec, rpy);
+      scr[21] = rpy[0];
+      scr[22] = rpy[1];
+      scr[23] = rpy[2];
+    }
+  }
+  wbar();
+  // ---- B: d_k,j = (Bdt u_k + Qdt f)_j + (Adt X_d,k-1)_j - X_d,k,j  (X_d,-1 = x0; component 12 = g)
+  {
+    const double* R = scr;
+    const double* Ii = scr + 9;
+    const float* traj = rec + CMPC_REC_HDR;
+    double dv[2] = {0.0, 0.0};
+#pragma unroll
+    for (int it = 0; it < 2; it++) {
+      const int t = 64 * wave + lane_opq() + it * G::NT;
+      if (t < 12 * N) {
+        const int k = t / 12, j = t - 12 * (t / 12);
+        const double* ts = scr + S0 + 12 * k;
+        const double xd = scr[18];
+        // w = B_c u_k (+ Q_c f: f_est(3) into row 9)
+        const double w9 = ts[3] * (1.0 / 12.0) + scr[19];
+        double c;
+        if (j < 3 || (j >= 6 && j < 9)) {
+          // j < 3: dt^2/2 (R' w[6:9])_j; 6..8: dt w_j, w[6:9] = I_w^-1 t
+          c = 0.0;
+#pragma unroll
+          for (int m = 0; m < 3; m++) {
+            const double wm = Ii[3 * m] * ts[0] + Ii[3 * m + 1] * ts[1] + Ii[3 * m + 2] * ts[2];
+            c += (j < 3) ? dth * R[3 * m + j] * wm : ((j - 6 == m) ? dt * wm : 0.0);
+          }
+        } else if (j == 3 || j == 9) {
+          c = ((j == 3) ? dth : dt) * w9;
+        } else if (j == 4 || j == 10) {
+          c = ((j == 4) ? dth : dt) * ts[4] * (1.0 / 12.0);
+        } else if (j == 5) {
+          c = dth * ts[5] * (1.0 / 12.0) + dt3 * xd * w9;
+        } else {
+          c = dt * ts[5] * (1.0 / 12.0) + dth * xd * w9;
+        }
+        // X_d,k-1 (x0 for k = 0: [rpy, p, w, v], rpy as quat_to_rpy in fp32)
+        auto vprev = [&](int i) -> double {
+          if (k > 0) return (double)traj[12 * (k - 1) + i];
+          if (i < 3) return scr[21 + i];
+          return (double)rec[(i < 6) ? CMPC_REC_P + i - 3 : (i < 9) ? CMPC_REC_W + i - 6 : CMPC_REC_V + i - 9];
+        };
+        double av = vprev(j);
+        if (j < 3) {
+          av += dt * (R[j] * vprev(6) + R[3 + j] * vprev(7) + R[6 + j] * vprev(8));
+        } else if (j < 6) {
+          av += dt * vprev(j + 6);
+          if (j == 5) av += dth * (xd * vprev(9) + scr[20]);
+        } else if (j == 11) {
+          av += dt * (xd * vprev(9) + scr[20]);
+        }
+        dv[it] = c + av - (double)traj[12 * k + j];
+      }
+    }
+    wbar();  // every read of t, s is done before the step slots are overwritten
+#pragma unroll
+    for (int it = 0; it < 2; it++) {
+      const int t = 64 * wave + lane_opq() + it * G::NT;
+      if (t < 12 * N) scr[S0 + t] = dv[it];
+    }
+  }
+  wbar();
+  // ---- C: wave 0, lane j < 12 owns component j of z, then of mu. Each step's coefficients are
+  // re-read from the LDS (R) and the kernel arguments: nothing but z / mu stays live
+  if (wave == 0) {
+    const int j = lane_opq();
+    const int jj = (j < 12) ? j : 11;
+    const double* R = scr;
+    float wf = 0.f;  // P.wts[jj] by uniform selects (a dynamic index would build a VGPR array)
+#pragma unroll
+    for (int i = 0; i < 12; i++) wf = (jj == i) ? P.wts[i] : wf;
+    // forward: z_j += (N1 z)_j + d_k,j   (N1 = Adt - I: rows 0..2 dt R' z[6:9], 3, 4 dt z9, z10,
+    // 5 dt z11 + dt^2/2 x_drag z9, 11 dt x_drag z9; z12 = 0)
+    double z = 0.0;
+    for (int k = 0; k < N; k++) {
+      const double dk = scr[S0 + 12 * k + jj];
+      const double z6 = rl_d(z, 6), z7 = rl_d(z, 7), z8 = rl_d(z, 8);
+      const double z9 = rl_d(z, 9), z10 = rl_d(z, 10), z11 = rl_d(z, 11);
+      double nz;
+      if (jj < 3) nz = dt * (R[jj] * z6 + R[3 + jj] * z7 + R[6 + jj] * z8);
+      else if (jj == 3) nz = dt * z9;
+      else if (jj == 4) nz = dt * z10;
+      else if (jj == 5) nz = dt * z11 + dth * scr[18] * z9;
+      else if (jj == 11) nz = dt * scr[18] * z9;
+      else nz = 0.0;
+      z += nz + dk;
+      if (j < 12) scr[S0 + 12 * k + j] = (double)wf * z;  // S e_k
+    }
+    // backward: mu_j += (N1' mu)_j + S e_k,j  (rows 6..8 dt R mu[0:3], 9 dt (mu3 + x_drag mu11) +
+    // dt^2/2 x_drag mu5, 10 dt mu4, 11 dt mu5)
+    double mu = 0.0;
+    for (int k = N - 1; k >= 0; k--) {
+      const double sk = scr[S0 + 12 * k + jj];
+      const double m0 = rl_d(mu, 0), m1 = rl_d(mu, 1), m2 = rl_d(mu, 2), m3 = rl_d(mu, 3);
+      const double m4 = rl_d(mu, 4), m5 = rl_d(mu, 5), m11 = rl_d(mu, 11);
+      double nm;
+      if (jj >= 6 && jj < 9) nm = dt * (R[3 * (jj - 6)] * m0 + R[3 * (jj - 6) + 1] * m1 + R[3 * (jj - 6) + 2] * m2);
+      else if (jj == 9) nm = dt * (m3 + scr[18] * m11) + dth * scr[18] * m5;
+      else if (jj == 10) nm = dt * m4;
+      else if (jj == 11) nm = dt * m5;
+      else nm = 0.0;
+      mu += nm + sk;
+      if (j < 12) scr[S0 + 12 * k + j] = mu;
+    }
+  }
+  wbar();
+  // ---- D: per step, y_k = I_w^-1 nu_k[6:9] and nu_k[9:12] / m into the step's first 6 slots
+  {
+    const int t = 64 * wave + lane_opq();
+    double ev = 0.0;
+    if (t < 6 * N) {
+      const int k = t / 6, i = t - 6 * (t / 6);
+      const double* mu = scr + S0 + 12 * k;
+      const double* R = scr;
+      const double* Ii = scr + 9;
+      const double xd = scr[18];
+      if (i < 3) {
+#pragma unroll
+        for (int m = 0; m < 3; m++) {
+          const double nu = dt * mu[6 + m] + dth * (R[3 * m] * mu[0] + R[3 * m + 1] * mu[1] + R[3 * m + 2] * mu[2]);
+          ev += Ii[3 * i + m] * nu;
+        }
+      } else if (i == 3) {
+        ev = (dt * mu[9] + dth * (mu[3] + xd * mu[11]) + dt3 * xd * mu[5]) * (1.0 / 12.0);
+      } else if (i == 4) {
+        ev = (dt * mu[10] + dth * mu[4]) * (1.0 / 12.0);
+      } else {
+        ev = (dt * mu[11] + dth * mu[5]) * (1.0 / 12.0);
+      }
+    }
+    wbar();
+    if (t < 6 * N) scr[S0 + 12 * (t / 6) + t - 6 * (t / 6)] = ev;
+  }
+  wbar();
+  // ---- E: row r's gradient entry, u = J2' r, x -= J2 u
+  float rr = 0.f;
+  {
+    CMPC_WIDE_IDS();
+    if (r < n) {
+      const int k = sh.varblk[r], c = sh.varcol[r];
+      const int b = c / 3, a = c - 3 * (c / 3);
+      const int a1 = (a == 2) ? 0 : a + 1, a2 = (a == 0) ? 2 : a - 1;
+      const double* yk = scr + 24 + 12 * k;
+      // (y x r_b)_a = y_a1 r_a2 - y_a2 r_a1
+      const double cr = yk[a1] * (double)rec[CMPC_REC_R + 4 * a2 + b] - yk[a2] * (double)rec[CMPC_REC_R + 4 * a1 + b];
+      rr = (float)(2.0 * (cr + yk[3 + a]) + (double)P.alpha2 * (double)xv);
+    }
+  }
+  float pa[NC], pb[NC];
+#pragma unroll
+  for (int m = 0; m < NC; m++) { pa[m] = 0.f; pb[m] = 0.f; }
+#ifndef CMPC_RB_NODPP
+  {
+    const int ln = lane_opq();
+    static_for<0, NH>([&](auto JC) {
+      constexpr int j = decltype(JC)::value;
+      float v = slot[j] * rr;
+      v += dppf<kDppQuadSwap1>(0.f, v);
+      v += dppf<kDppQuadSwap2>(0.f, v);
+      v += dppf<kDppRowHalfMirror>(0.f, v);
+      v += dppf<kDppRowMirror>(0.f, v);
+      v += dppf<kDppRowBcast15, 0xa>(0.f, v);  // rows 1 / 3 += row 0 / 2: the two halves' sums
+      const float s0 = rl(v, 31), s1 = rl(v, 63);
+      if (ln == (j & 63)) { pa[j >> 6] = s0; pb[j >> 6] = s1; }
+      if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    });
+    // the waves' partials summed in wave order, masked to the columns q <= l < n
+    float* ub = sh.vbuf();
+    for (int w = 0; w < G::NW; w++) {
+      if (wave == w) {
+        const bool last = (w == G::NW - 1);
+#pragma unroll
+        for (int m = 0; m < NC; m++) {
+          const int l = 64 * m + ln;
+          if (l < NH) {
+            float u0 = pa[m] + (w ? ub[l] : 0.f);
+            float u1 = pb[m] + (w ? ub[G::HOFF + l] : 0.f);
+            if (last) {
+              u0 = (l >= q && l < n) ? u0 : 0.f;
+              u1 = (NH + l >= q && NH + l < n) ? u1 : 0.f;
+            }
+            ub[l] = u0;
+            ub[G::HOFF + l] = u1;
+          }
+        }
+      }
+      wbar();
+    }
+  }
+#endif
+  {
+    CMPC_WIDE_IDS();
+    f2v acc = {0.f, 0.f};
+    const float* vb = &sh.vbuf()[h * G::HOFF];
+#pragma unroll
+    for (int j = 0; j < NH; j += 4) {
+      const float4 u4 = *reinterpret_cast<const float4*>(vb + j);
+      dot4(acc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], u4);
+      CMPC_WSWEEP_FENCE(j);
+    }
+    const float dx = pair_sum(acc.x + acc.y);
+    if (r < n) xv -= dx;
+  }
+}
 
 template <int NV>
 __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KParams& P,
@@ -604,6 +918,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   Cons cp{};
   float up = 0.f;
   if (status == CMPC_OK && CMPC_DIAG_STOP == 0) {
+   for (int pass = 0;; pass++) {
     for (;;) {
       wpin(slot);
       CMPC_WIDE_IDS();
@@ -984,6 +1299,12 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         q--;
       }
     }
+    // converged: one refinement step (from N = 11), then the constraints are checked again (a
+    // step that violates one continues the dual active set from the refined point)
+    if (pass > 0 || !(CMPC_WIDE_REFINE && P.refine) || status != CMPC_OK) break;
+    rinv_ok = false;  // the R^-1 area is the refinement's scratch from here on
+    wide_refine<NV>(rec, P, sh, slot, xv, q, n, wave);
+   }
   }
 
   // ---- scatter (q_soln layout 12 k + 3 leg + axis, swing -> 0) staged in LDS, coalesced out

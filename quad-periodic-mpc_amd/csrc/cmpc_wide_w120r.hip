@@ -1,0 +1,18 @@
+// cmpc_wide_w120r.hip — the 120-column wide class with the fp64 refinement step of the converged
+// active set (cmpc_wide.h wide_refine; horizons N > 10), one workgroup per list entry.
+#ifndef CMPC_WIDE_WAVES_PER_EU
+#define CMPC_WIDE_WAVES_PER_EU 4
+#endif
+#define CMPC_WIDE_BUILD 1
+#define CMPC_WIDE_REFINE 1
+#include "cmpc_wide.h"
+
+namespace cmpc {
+
+hipError_t launch_wide_w120_r(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
+                            int32_t* d_iters, const int* in_list, const int* in_count, int* deq, int grid,
+                            hipStream_t stream) {
+  return launch_wide_impl<120>(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid, stream);
+}
+
+}  // namespace cmpc

@@ -7,13 +7,27 @@
 #ifndef CMPC_WIDE_BUILD
 #define CMPC_WIDE_BUILD 1  // one workgroup per entry here; the persistent form in cmpc_wide_w96p.hip
 #endif
+#ifndef CMPC_WIDE_REFINE
+#define CMPC_WIDE_REFINE 0  // N <= 10 (no refinement); the refining builds: cmpc_wide_w96r.hip, w96pr.hip
+#endif
 #include "cmpc_wide.h"
 
 namespace cmpc {
 
+// the same class with the fp64 refinement step (N > 10), each launch form in its own unit
+hipError_t launch_wide_w96_r(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
+                            int32_t* d_iters, const int* in_list, const int* in_count, int* deq, int grid,
+                            hipStream_t stream);
+hipError_t launch_wide_w96_persist_r(const float* d_recs, const KParams& P, float* d_forces,
+                                    uint8_t* d_status, int32_t* d_iters, const int* in_list,
+                                    const int* in_count, int* deq, int grid, hipStream_t stream);
+
 hipError_t launch_wide_w96(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
                           int32_t* d_iters, const int* in_list, const int* in_count, int* deq, int grid,
                           hipStream_t stream) {
+  if (P.refine)
+    return deq ? launch_wide_w96_persist_r(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid, stream)
+               : launch_wide_w96_r(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, nullptr, grid, stream);
   if (deq)  // persistent form: its own unit (compiled beside this kernel it spilled registers)
     return launch_wide_w96_persist(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid,
                                    stream);

@@ -4,6 +4,9 @@
 #define CMPC_WIDE_WAVES_PER_EU 5
 #endif
 #define CMPC_WIDE_BUILD 2
+#ifndef CMPC_WIDE_REFINE
+#define CMPC_WIDE_REFINE 0  // N <= 10; the refining persistent build: cmpc_wide_w96pr.hip
+#endif
 #include "cmpc_wide.h"
 
 namespace cmpc {

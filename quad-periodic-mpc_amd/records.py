@@ -21,7 +21,7 @@ REC_XDRAG = 28   # x_drag
 REC_FEST3 = 29   # f_est(3) compensation force (config 5)
 REC_FLAGS = 30   # uint32 bit-cast; bit 0: use f_est in qg
 REC_HDR = 32
-MAX_HORIZON = 24
+MAX_HORIZON = 20
 # config 5 (include/cmpc_solver.h CMPC_LOG_* / CMPC_EST_*)
 LOG_POS, LOG_EUL, LOG_ANG, LOG_LIN, LOG_FORCE, LOG_XDRAG, LOG_R, LOG_ROT = 0, 3, 6, 9, 12, 24, 25, 37
 LOG_WORDS = 48

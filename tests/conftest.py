@@ -41,7 +41,7 @@ def golden_params(cm, g):
 
 GOLDEN_SETS = ["n10_mixed", "n10_stress", "n10_edge", "n16_trot", "n19_mixed", "n20_trot",
                "n20_mixed", "n12_allstance", "n16_standing", "n20_standing", "n16_walking",
-               "n20_walking", "n22_standing", "n24_standing"]
+               "n20_walking"]
 
 
 def rel_force_err(f, f_ref):

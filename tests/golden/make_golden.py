@@ -87,9 +87,6 @@ SETS = {
     "n20_standing": lambda: (gait_set(8, 20, 1011, "standing"), cm.make_params(20), 0),
     "n16_walking": lambda: (gait_set(8, 16, 1012, "walking"), cm.make_params(16), 0),
     "n20_walking": lambda: (gait_set(8, 20, 1013, "walking"), cm.make_params(20), 0),
-    # class G (n > 256): standing at N = 22 (n = 264) and N = 24 (n = 288, CMPC_MAX_HORIZON)
-    "n22_standing": lambda: (gait_set(4, 22, 1014, "standing"), cm.make_params(22), 0),
-    "n24_standing": lambda: (gait_set(4, 24, 1015, "standing"), cm.make_params(24), 0),
 }
 
 

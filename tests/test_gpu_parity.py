@@ -119,9 +119,9 @@ def test_edge_cases(cm, solver_mod):
 
 # (N, stress, random-contact fraction, gait, batch). The controller's gaits
 # (ConvexMPCLocomotion.cpp:41-51): standing puts every foot in stance (n = 12 N: the 192-column
-# class at N = 16, 256 at N = 20, class G at N = 22 / 24), walking three feet (n = 138-141 at
-# N = 16: the 144 class; 180 at N = 20: 192). N = 17..19 random contacts: the horizons the
-# reference admits beyond the deployed one, held strictly.
+# class at N = 16, 256 at N = 20, the largest reduced QP CMPC_MAX_HORIZON = 20 admits), walking
+# three feet (n = 138-141 at N = 16: the 144 class; 180 at N = 20: 192). N = 17..19 random
+# contacts: the horizons the reference admits beyond the deployed one, held strictly.
 LIVE_CASES = [(10, False, 0.25, "trotting", 512), (10, True, 0.25, "trotting", 512),
               (10, False, 1.0, "trotting", 512), (5, False, 0.25, "trotting", 512),
               (16, False, 0.0, "trotting", 512), (1, False, 0.5, "trotting", 512),
@@ -130,8 +130,7 @@ LIVE_CASES = [(10, False, 0.25, "trotting", 512), (10, True, 0.25, "trotting", 5
               (19, True, 0.25, "trotting", 512),
               (16, False, 0.0, "standing", 512), (20, False, 0.0, "standing", 512),
               (16, False, 0.0, "walking", 512), (20, False, 0.0, "walking", 512),
-              (16, True, 0.0, "standing", 256),
-              (22, False, 0.0, "standing", 128), (24, False, 0.0, "standing", 128)]
+              (16, True, 0.0, "standing", 256)]
 
 
 @pytest.mark.parametrize("N,stress,frac,gait,B", LIVE_CASES)

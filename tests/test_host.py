@@ -88,3 +88,42 @@ def test_library_exports_header_symbols(cm):
     lib = ctypes.CDLL(path)  # loads without a GPU
     lib.cmpc_record_words.argtypes = [ctypes.c_int]
     assert lib.cmpc_record_words(10) == cm.record_words(10)
+
+
+def test_gait_tables_match_offset_duration_rule(cm):
+    """The controller's other OffsetDurationGaits (ConvexMPCLocomotion.cpp:41-51) through the
+    generator: standing puts every foot in stance, walking follows (row - offset) mod P <
+    duration (Gait.cpp:159-188)."""
+    from importlib import import_module
+    inst = import_module("quad-periodic-mpc_amd.instances")
+    tabs = inst.loco_gaits(18)
+    it = np.arange(18)
+    for name in ("standing", "walking", "bounding", "galloping"):
+        off, dur, _ = tabs[name]
+        tab = inst.gait_table(10, it, off, dur, 18).reshape(18, 10, 4)
+        for i0 in range(18):
+            for i in range(10):
+                row = (i + i0 + 1) % 18
+                assert list(tab[i0, i].astype(bool)) == [(row - o) % 18 < d for o, d in zip(off, dur)]
+    recs = cm.make_instances(64, 16, random_contact_frac=0.0, gait="standing")
+    assert (cm.unpack_gait(recs, 16) == 1).all()
+    recs = cm.make_instances(64, 16, random_contact_frac=0.0, gait="walking")
+    n = 3 * (cm.unpack_gait(recs, 16) != 0).sum(1)
+    assert set(np.unique(n)) <= {138, 141}
+
+
+def test_horizon_beyond_max_is_rejected(cm):
+    """CMPC_MAX_HORIZON = 20 (the reference's 19, lifted by one for config 5): longer horizons
+    are refused by the host mirror and by the library (before any HIP call)."""
+    from importlib import import_module
+    solver = import_module("quad-periodic-mpc_amd.solver")
+    with pytest.raises(ValueError):
+        cm.make_params(21)
+    if not os.path.exists(solver.LIB_PATH):
+        pytest.skip("libcmpc_hip.so not built")
+    lib = solver.load_library()
+    prm = cm.make_params(20)
+    prm.horizon = 21
+    h = ctypes.c_void_p()
+    assert lib.cmpc_batch_create(ctypes.byref(h), ctypes.byref(prm), 16, None) == -2
+    assert b"horizon" in lib.cmpc_last_error()
