@@ -150,7 +150,7 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
   // of class 1's queue, so they finish inside class 1's run instead of forming a tail
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (const char* pe = getenv("CMPC_SIDE_PRIORITY"); pe && atoi(pe) == 0) prio_hi = prio_lo;
+  if (cmpc::diag_knob("CMPC_SIDE_PRIORITY", 1) == 0) prio_hi = prio_lo;
   for (int j = 0; j < cmpc::kSideStreams; j++) {
     e = hipStreamCreateWithPriority(&h->ctx.side[j], hipStreamNonBlocking, prio_hi);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.join[j], hipEventDisableTiming);

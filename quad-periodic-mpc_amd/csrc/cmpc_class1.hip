@@ -858,12 +858,9 @@ hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& 
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,
                          int* ovf_list, int* ovf_count, int grid, hipStream_t stream) {
   if (grid <= 0) return hipSuccess;
-  // CMPC_C1_DYN_LDS=<bytes> (diagnostic): extra dynamic LDS per workgroup, i.e. fewer class-1
+  // CMPC_C1_DYN_LDS=<bytes> (diagnostic build only): extra dynamic LDS per workgroup, i.e. fewer class-1
   // workgroups per CU (placement / occupancy experiments)
-  static const unsigned dyn = [] {
-    const char* e = getenv("CMPC_C1_DYN_LDS");
-    return e ? (unsigned)atoi(e) : 0u;
-  }();
+  static const unsigned dyn = (unsigned)diag_knob("CMPC_C1_DYN_LDS", 0);
   if (nv == 60)
     hipLaunchKernelGGL(cmpc_solve_c1_kernel<60>, dim3(grid), dim3(64), dyn, stream, d_recs, batch, P,
                        d_forces, d_status, d_iters, in_list, in_count, ovf_list, ovf_count);

@@ -2,10 +2,24 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/cmpc_solver.h"
 
 namespace cmpc {
+
+// Launch-placement knobs of the A/B experiments: read from the environment only
+// in a diagnostic build (-DCMPC_DIAG_KNOBS=1, scripts/build_diag_variant.sh); the product build
+// always runs the measured defaults.
+inline int diag_knob(const char* name, int dflt) {
+#if defined(CMPC_DIAG_KNOBS) && CMPC_DIAG_KNOBS
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
 
 // Kernel-side copy of cmpc_params (by value, lands in SGPRs).
 struct KParams {

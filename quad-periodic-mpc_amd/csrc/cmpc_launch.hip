@@ -68,10 +68,7 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
 // (config 2: 11.3 M -> 11.7 M QP/s).
 // CMPC_WIDE_FORM (A/B): 1 every class one-per-entry, 2 every class persistent.
 bool one_per_entry(int lo, int hi, int N, int batch) {
-  static const int form = [] {
-    const char* v = getenv("CMPC_WIDE_FORM");
-    return v ? atoi(v) : 0;
-  }();
+  static const int form = diag_knob("CMPC_WIDE_FORM", 0);
   if (form == 1 || batch < 16384) return true;
   if (form == 2) return false;
   const float mode = 6.f * (float)N, half = 3.f * sqrtf((float)N);
@@ -79,6 +76,16 @@ bool one_per_entry(int lo, int hi, int N, int batch) {
 }
 
 }  // namespace
+
+// Grid of the 80-column class when it is launched ahead of class 1 (0: off). At N <= 10 class 1
+// holds the trot size and carries the batch; its one-wave workgroups take every wave slot a CU
+// frees, so the three-wave 80-column workgroups of the random-contact instances were dispatched
+// late and ended 0.3 ms after class 1 (round-3 kernel trace). Ahead: classify first on the
+// handle's stream, then a persistent 80-column grid of this many workgroups (resident before class
+// 1 starts) dequeues that class's list while class 1 fills the rest of the GPU.
+#ifndef CMPC_WIDE_AHEAD
+#define CMPC_WIDE_AHEAD 0
+#endif
 
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
@@ -106,11 +113,11 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // on the handle's stream ahead of everything. Batch sweep of both placements with the final
     // kernels (profiles/r03_ab/sweep2): beside class 1 +2 % at 16384 .. 131072 instances, within
     // noise below. CMPC_CLASSIFY_SIDE=0/1 forces either placement (A/B).
-    static const int cls_env = [] {
-      const char* v = getenv("CMPC_CLASSIFY_SIDE");
-      return v ? atoi(v) : -1;
-    }();
-    const bool cls_side = (cls_env < 0) ? (batch >= 16384) : (cls_env == 1);
+    static const int cls_env = diag_knob("CMPC_CLASSIFY_SIDE", -1);
+    // the 80-column class ahead of class 1 (CMPC_WIDE_AHEAD): large batches whose class 1 holds
+    // the trot size (6 N <= 60)
+    const bool ahead = CMPC_WIDE_AHEAD > 0 && batch >= 16384 && 6 * P.N <= 60;
+    const bool cls_side = ahead ? false : (cls_env < 0) ? (batch >= 16384) : (cls_env == 1);
     hipStream_t cs = cls_side ? ctx.side[0] : stream;
     if (cls_side) {
       if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
@@ -128,10 +135,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // surplus workgroups exit after one load. CMPC_EXACT_GRID=1 (diagnostic): read the list
     // lengths back first (a host round trip per solve) and launch exact grids. Measured: +1 % at
     // config 3, +0.2 % at config 5 (where the 256-row class launches only empty workgroups)
-    static const bool exact = [] {
-      const char* v = getenv("CMPC_EXACT_GRID");
-      return v && v[0] == '1';
-    }();
+    static const bool exact = diag_knob("CMPC_EXACT_GRID", 0) == 1;
     if (exact) {
       static int* h_cnt = nullptr;
       if (!h_cnt && (e = hipHostMalloc(reinterpret_cast<void**>(&h_cnt), kHdr * sizeof(int))) != hipSuccess)
@@ -153,7 +157,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       return e;
     // side 0: 80, 120, 144, 256; side 1: 96, 128, 192 (at N = 20 the 120-column class, which
     // carries the batch, runs beside the 128-column class)
-    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1], dq(0, 65, 80), grid_of[0],
+    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1],
+                             ahead ? &cnt[kDeq + 0] : dq(0, 65, 80), ahead ? CMPC_WIDE_AHEAD : grid_of[0],
                              ctx.side[0])) != hipSuccess)
       return e;
     if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], dq(1, 81, 96),
@@ -171,10 +176,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // by side instead of back to back. Config 5 4.21 M -> 4.41 M QP/s against both on side 1
     // (profiles/r03_ab/sparse_side). CMPC_SPARSE_SIDE (A/B): the side streams of the 144 / 192
     // classes as two digits (11 = both on side 1)
-    static const int sparse_side = [] {
-      const char* v = getenv("CMPC_SPARSE_SIDE");
-      return v ? atoi(v) : 1;
-    }();
+    static const int sparse_side = diag_knob("CMPC_SPARSE_SIDE", 1);
     if (n_max > 128 &&
         (e = launch_wide_w144(d_recs, P, d_forces, d_status, d_iters, list[6], &cnt[7], &cnt[kDeq + 6], grid_of[6],
                               ctx.side[(sparse_side / 10) & 1])) != hipSuccess)
