@@ -370,10 +370,8 @@ def scaling_model(args, cm, dev, sync):
     out_b = 4 * 12 * N
     recs_all = torch.from_numpy(cm.make_instances(G_total, N, random_contact_frac=args.random_contact_frac)).to(dev)
     rows, t1 = [], None
-    for G in (1, 2, 4, 8):
-        local = G_total // G
-        # the pieces a G-rank run cuts each rank's shard into (world 1 itself solves in one piece)
-        pipe = par.RootPipeline(prm, local, chunks=par.auto_chunks(local, G), device=dev)
+    def timed_pieces(local, chunks):
+        pipe = par.RootPipeline(prm, local, chunks=chunks, device=dev)
         recs = recs_all[:local]
         for _ in range(3):
             pipe.step(recs)
@@ -383,11 +381,21 @@ def scaling_model(args, cm, dev, sync):
         for _ in range(steps):
             pipe.step(recs)
         sync()
-        t_solve = (time.perf_counter() - t0) / steps
-        pieces = pipe.sizes
+        t = (time.perf_counter() - t0) / steps
+        sizes = pipe.sizes
         pipe.close()
+        return t, sizes
+
+    for G in (1, 2, 4, 8):
+        local = G_total // G
+        # the pieces a G-rank run cuts each rank's shard into (world 1 itself solves in one piece)
+        t_solve, pieces = timed_pieces(local, par.auto_chunks(local, G))
         row = {"gpus": G, "per_rank_instances": local, "pieces": len(pieces),
                "piece_instances": pieces[0], "t_solve_ms_measured": round(t_solve * 1e3, 4)}
+        if G > 1:   # the other piece count, for comparison (pieces alternate over two handles)
+            alt = 1 if len(pieces) > 1 else 2
+            t_alt, _ = timed_pieces(local, alt)
+            row["t_solve_ms_measured_with_%d_pieces" % alt] = round(t_alt * 1e3, 4)
         if G == 1:
             t1 = t_solve
             row.update(t_model_ms=round(t_solve * 1e3, 4), speedup=1.0)
@@ -526,7 +534,7 @@ def main():
         for _ in range(args.warmup):
             step()
         sync()
-        timed = None if args.dry_run else pipe._solver
+        timed = None if args.dry_run else pipe   # per-launch events on every lane's handle
         units_per_launch = max(pipe.sizes)
         if timed is not None:
             timed.enable_timing(args.steps * pipe.chunks)

@@ -95,6 +95,13 @@ struct C1Geo {
   }
   // prow(r) - (r & ~3): element (r, c) lives at prow0(r) + c
   __host__ __device__ static constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+  // H's exchange between the condensation and the row loads: the plain packed upper triangle,
+  // element (r, c >= r) at tri(r) + c. Lane v stores its row and loads the entries c >= v at
+  // tri(v) + c: with these unaligned row starts the lanes of a half-wave hit distinct banks
+  // (with the 16-B aligned rows of prow, which the Cholesky's ds_read_b128 broadcasts need, only
+  // 16 bank groups: 650 -> 215 extra LDS cycles per instance at NV = 60 by a bank model)
+  __host__ __device__ static constexpr int tri(int r) { return r * NV - ((r * (r + 1)) >> 1); }
+  static_assert(NV * NV - ((NV * (NV + 1)) >> 1) <= 4 * NG * NV - 8 * NG * (NG - 1), "exchange fits P");
 };
 // R (upper triangular, q x q) packed by columns: R[i][j] at rcol(j) + i, i <= j
 __device__ __forceinline__ int rcol(int j) { return (j * (j + 1)) >> 1; }
@@ -297,7 +304,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       gv = real ? 2.f * dot13(b, zk) : 0.f;  // qg = 2 B_qp' S (A_qp x0 + Q_qp f - X_d)
     }
     lsync();  // every ZE read is issued before P is overwritten
-    const int myrow = G::prow0(v);
+    const int myrow = G::tri(v);
     float z[13];
 #pragma unroll
     for (int j = 0; j < 13; j++) z[j] = 0.f;
@@ -325,10 +332,10 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   float slot[NV + 1];
   {
     const int vv = (v < NV) ? v : 0;  // lanes without a row read row 0 (and keep a zero row)
-    const int myrow = G::prow0(vv);
+    const int myrow = G::tri(vv);
     static_for<0, NV>([&](auto C) {
       constexpr int c = decltype(C)::value;
-      const int addr = (c >= vv) ? myrow + c : G::prow0(c) + vv;
+      const int addr = (c >= vv) ? myrow + c : G::tri(c) + vv;
       const float x = sh.P[addr];
       slot[c] = (real && c < n) ? x : ((c == v) ? 1.f : 0.f);
       if ((c & 7) == 7) __builtin_amdgcn_sched_barrier(0);

@@ -76,6 +76,10 @@ struct WGeo {
     return 4 * (r >> 2) * NV - 8 * (r >> 2) * ((r >> 2) - 1) + (r & 3) * (NV - 4 * (r >> 2));
   }
   __host__ __device__ static constexpr int prow0(int r) { return prow(r) - (r & ~3); }
+  // H's exchange between the condensation and the row loads: the plain packed upper triangle,
+  // element (r, c >= r) at tri(r) + c (unaligned row starts spread a half-wave's rows over the
+  // banks; the 16-B aligned prow rows gave 16 bank groups)
+  __host__ __device__ static constexpr int tri(int r) { return r * NV - ((r * (r + 1)) >> 1); }
   // factor rows: row k = even-column segment then odd-column segment, columns 2 j0(k) + h on
   __host__ __device__ static constexpr int j0(int k) { return (k >> 1) & ~3; }
   __host__ __device__ static constexpr int seg(int k) {  // segment stride (words)
@@ -650,7 +654,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
       gv = real ? 2.f * dot13(b, zk) : 0.f;  // qg = 2 B_qp' S (A_qp x0 + Q_qp f - X_d)
     }
     wbar();  // every ZE read is done before P is overwritten
-    const int myrow = G::prow0(rr);
+    const int myrow = G::tri(rr);
     float z[13];
 #pragma unroll
     for (int j = 0; j < 13; j++) z[j] = 0.f;
@@ -687,11 +691,11 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   float slot[NH];
   float gb = gv;  // border: g_r, then y_r (both halves keep it)
   {
-    const int myrow = G::prow0(rr);
+    const int myrow = G::tri(rr);
     static_for<0, NH>([&](auto J) {
       constexpr int j = decltype(J)::value;
       const int c = 2 * j + h;
-      const int addr = (c >= rr) ? myrow + c : G::prow0(c) + rr;
+      const int addr = (c >= rr) ? myrow + c : G::tri(c) + rr;
       const float x = sh.P[addr];
       slot[j] = (real && c < n) ? x : ((c == r) ? 1.f : 0.f);
       if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);

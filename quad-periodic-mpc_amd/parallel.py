@@ -197,12 +197,20 @@ class RootPipeline:
     scatter 0, scatter 1, gather 0, scatter 2, gather 1, ... — a gather never delays the next
     piece's scatter.
 
-    ``solve_fn(records, forces, status)`` solves rows in place (device tensors of this rank);
-    the default binds a :class:`BatchSolver` to the current stream. Every buffer is allocated
+    ``solve_fn(records, forces, status)`` solves rows in place (device tensors of this rank).
+    The default solves the pieces on ``lanes`` (two) :class:`BatchSolver` handles, each on its
+    own stream, alternating: piece c + 1's solve (its class-1 launch) starts while piece c's
+    slowest instances (the wide size classes) are still running, instead of queueing behind
+    piece c's join, and piece c's gather waits for piece c's solve only. Each handle has its own
+    work lists, so the overlapping solves never share scratch; every piece is still solved by
+    the same kernels, so the forces are bitwise those of one solve. Every buffer is allocated
     here, none inside :meth:`step`."""
 
+    LANES = 2   # solver handles (streams) the pieces alternate over
+
     def __init__(self, params, global_batch: int, chunks: Optional[int] = None, *, group=None,
-                 device=None, src: int = 0, solve_fn=None, record_words: Optional[int] = None):
+                 device=None, src: int = 0, solve_fn=None, record_words: Optional[int] = None,
+                 lanes: Optional[int] = None):
         from .records import record_words as _rw
         self.params = params
         self.N = params.horizon
@@ -248,25 +256,65 @@ class RootPipeline:
                         self._root_recv[(r, c)] = torch.zeros((S, cols), dtype=torch.float32, device=dev)
         self._solve_fn = solve_fn
         self._solver = None
+        self._solvers = []
+        self._streams = []
         if solve_fn is None:
             import importlib
             solver_mod = importlib.import_module(__package__ + ".solver")
-            stream = torch.cuda.current_stream(dev)
-            self._solver = solver_mod.BatchSolver(params, max_batch=max(1, max(self.sizes)),
-                                                  stream=stream)
+            nl = max(1, min(self.LANES if lanes is None else int(lanes), self.chunks))
+            self._streams = [torch.cuda.Stream(dev) for _ in range(nl)]
+            self._solvers = [solver_mod.BatchSolver(params, max_batch=max(1, max(self.sizes)), stream=st)
+                             for st in self._streams]
+            self._solver = self._solvers[0]
+
+    def _lane(self, c):
+        """(solver, stream) of piece c (None, None with a solve_fn)."""
+        if not self._solvers:
+            return None, None
+        k = c % len(self._solvers)
+        return self._solvers[k], self._streams[k]
+
+    def enable_timing(self, steps: int) -> None:
+        """Per-launch HIP events on every handle for the next ``steps`` solves of each."""
+        for sv in self._solvers:
+            sv.enable_timing(steps)
+
+    def read_timing(self):
+        """(ms [solves, 2] over all handles, wide-class count of handle 0's last solve)."""
+        import numpy as np
+        if not self._solvers:
+            return np.zeros((0, 2)), 0
+        parts = [sv.read_timing() for sv in self._solvers]
+        return np.concatenate([p[0] for p in parts], 0), parts[0][1]
 
     def _local(self, c):
         a, b = self.plan[self.rank][c]
         return a - self.start, b - self.start
 
-    def _solve_piece(self, c):
+    def _solve_piece(self, c, recs=None, forces=None, status=None):
+        """Solve piece c (this rank's rows of it, or the given rows) on its lane: the lane's
+        stream is the current one when this runs (step / solve_only arrange that)."""
         a, b = self._local(c)
         if b <= a:
             return
+        recs = self.local_recs[a:b] if recs is None else recs
+        forces = self.local_forces[a:b] if forces is None else forces
+        status = self.local_status[a:b] if status is None else status
         if self._solve_fn is not None:
-            self._solve_fn(self.local_recs[a:b], self.local_forces[a:b], self.local_status[a:b])
+            self._solve_fn(recs, forces, status)
         else:
-            self._solver.solve(self.local_recs[a:b], self.local_forces[a:b], self.local_status[a:b])
+            self._lane(c)[0].solve(recs, forces, status)
+
+    def _fork(self):
+        """Every lane stream waits for the caller's stream (inputs ready, earlier work done)."""
+        cur = torch.cuda.current_stream(self.device) if self._streams else None
+        for st in self._streams:
+            st.wait_stream(cur)
+        return cur
+
+    def _join(self, cur):
+        for st in self._streams:
+            cur.wait_stream(st)
 
     def _scatter(self, records_root, c):
         S = self.sizes[c]
@@ -319,12 +367,15 @@ class RootPipeline:
                                       tuple(records_root.shape) != (self.batch, self.words)):
             raise ValueError(f"root must pass records of shape ({self.batch}, {self.words})")
         C = self.chunks
+        cur = self._fork()
         if self.world == 1:   # nothing to move: solve the resident records in place
             for c in range(C):
                 a, b = self.plan[0][c]
                 if b > a:
-                    fn = self._solve_fn or self._solver.solve
-                    fn(records_root[a:b], self.forces[a:b], self.local_status[a:b])
+                    with _on(self._lane(c)[1]):
+                        self._solve_piece(c, records_root[a:b], self.forces[a:b], self.local_status[a:b])
+            if cur is not None:
+                self._join(cur)
             return
         sc = [None] * C
         ga = [None] * C
@@ -332,23 +383,48 @@ class RootPipeline:
         for c in range(C):
             if c + 1 < C:
                 sc[c + 1] = self._scatter(records_root, c + 1)
-            sc[c].wait()
-            if c in self._recv:
-                a, b = self._local(c)
-                self.local_recs[a:b].copy_(self._recv[c][:b - a])
-            self._solve_piece(c)
-            ga[c] = self._gather(c)
+            # on piece c's lane: wait for its scatter, solve, then its gather (the collective
+            # waits for this stream, i.e. for piece c's solve, not for the other lane's)
+            with _on(self._lane(c)[1]):
+                sc[c].wait()
+                if c in self._recv:
+                    a, b = self._local(c)
+                    self.local_recs[a:b].copy_(self._recv[c][:b - a])
+                self._solve_piece(c)
+                ga[c] = self._gather(c)
         for c in range(C):
             self._finish_gather(c, ga[c])
+        if cur is not None:
+            self._join(cur)
 
     def solve_only(self) -> None:
         """The same pieces solved with no collective (kernel-only rate of the shard)."""
         if self.world == 1:
             return self.step(self._last_root)
+        cur = self._fork()
         for c in range(self.chunks):
-            self._solve_piece(c)
+            with _on(self._lane(c)[1]):
+                self._solve_piece(c)
+        if cur is not None:
+            self._join(cur)
 
     def close(self):
-        if self._solver is not None:
-            self._solver.close()
-            self._solver = None
+        for sv in self._solvers:
+            sv.close()
+        self._solvers = []
+        self._solver = None
+
+
+class _on:
+    """``torch.cuda.stream(st)`` when st is a stream, else a no-op (CPU ranks, solve_fn)."""
+
+    def __init__(self, st):
+        self.ctx = torch.cuda.stream(st) if st is not None else None
+
+    def __enter__(self):
+        if self.ctx is not None:
+            self.ctx.__enter__()
+
+    def __exit__(self, *a):
+        if self.ctx is not None:
+            self.ctx.__exit__(*a)
