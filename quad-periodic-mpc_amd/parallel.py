@@ -262,17 +262,22 @@ class RootPipeline:
             import importlib
             solver_mod = importlib.import_module(__package__ + ".solver")
             nl = max(1, min(self.LANES if lanes is None else int(lanes), self.chunks))
-            self._streams = [torch.cuda.Stream(dev) for _ in range(nl)]
-            self._solvers = [solver_mod.BatchSolver(params, max_batch=max(1, max(self.sizes)), stream=st)
-                             for st in self._streams]
+            if nl == 1:   # one lane: the caller's stream itself (no fork / join)
+                self._solvers = [solver_mod.BatchSolver(params, max_batch=max(1, max(self.sizes)),
+                                                        stream=torch.cuda.current_stream(dev))]
+            else:
+                self._streams = [torch.cuda.Stream(dev) for _ in range(nl)]
+                self._solvers = [solver_mod.BatchSolver(params, max_batch=max(1, max(self.sizes)), stream=st)
+                                 for st in self._streams]
             self._solver = self._solvers[0]
 
     def _lane(self, c):
-        """(solver, stream) of piece c (None, None with a solve_fn)."""
+        """(solver, stream) of piece c: stream None means the caller's current stream (one lane,
+        or a solve_fn)."""
         if not self._solvers:
             return None, None
         k = c % len(self._solvers)
-        return self._solvers[k], self._streams[k]
+        return self._solvers[k], (self._streams[k] if self._streams else None)
 
     def enable_timing(self, steps: int) -> None:
         """Per-launch HIP events on every handle for the next ``steps`` solves of each."""
