@@ -67,12 +67,21 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
 // (the same threshold as class 1's split) the drains are short and every class is one-per-entry
 // (config 2: 11.3 M -> 11.7 M QP/s).
 // CMPC_WIDE_FORM (A/B): 1 every class one-per-entry, 2 every class persistent.
+// the one-workgroup-per-entry launch form only for the class that holds 6 N itself (1), or for
+// every class meeting 6 N +- 3 sqrt(N) (0, round 3)
+#ifndef CMPC_POPULOUS_EXACT
+#define CMPC_POPULOUS_EXACT 0
+#endif
 bool one_per_entry(int lo, int hi, int N, int batch) {
   static const int form = diag_knob("CMPC_WIDE_FORM", 0);
   if (form == 1 || batch < 16384) return true;
   if (form == 2) return false;
+#if CMPC_POPULOUS_EXACT
+  return lo <= 6 * N && 6 * N <= hi;  // only the class holding the trot size itself
+#else
   const float mode = 6.f * (float)N, half = 3.f * sqrtf((float)N);
   return (float)hi >= mode - half && (float)lo <= mode + half;
+#endif
 }
 
 }  // namespace

@@ -105,7 +105,12 @@ struct WGeo {
   static constexpr int GI_END = O_CS + 2 * NV + 8;
   // R^-1 beside R for the first QI active-set positions (sized to keep each class's workgroups
   // per CU: 80 / 96 six, 120 / 128 four)
-  static constexpr int QI = (NV == 80) ? 56 : (NV == 96) ? 40 : (NV == 120) ? 48 : (NV == 128) ? 32 : 64;
+#ifdef CMPC_WIDE_QI
+  static constexpr int QI = CMPC_WIDE_QI;
+#else
+  static constexpr int QI = (NV == 80) ? 56 : (NV == 96) ? 40 : (NV == 120) ? 48 : (NV == 128) ? 32
+                            : (NV == 144) ? 40 : 64;
+#endif
   static constexpr int O_RINV = (GI_END + 3) & ~3;
   static constexpr int PTOT = (mx(mx(PSZ + 12 * 16, PSZ + CH), O_RINV + QI * (QI + 1) / 2) + 3) & ~3;
   // the refinement's fp64 scratch (refine_gradient_seq: 18 + 12 N doubles) in the R^-1 area,
