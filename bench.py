@@ -287,7 +287,8 @@ def carrying_wide_kernel(N: int) -> str:
     trot workloads, the mode of any contact mix): launched one workgroup per list entry
     (cmpc_launch.hip one_per_entry), hence the `false` (not persistent) template argument."""
     nv = next(v for v in WIDE_CLASS_NV if v >= 6 * N)
-    return f"cmpc_solve_w_kernel<{nv}, false>"
+    # the refining builds (fp64 refinement of the active set) serve N > 10
+    return f"cmpc_solve_w_kernel<{nv}, false, {'true' if N > 10 else 'false'}>"
 
 
 def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):

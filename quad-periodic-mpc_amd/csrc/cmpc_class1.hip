@@ -718,7 +718,6 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         // R and re-triangularise rows kk..q-1 (lane c rebuilds column c of R in place: every
         // read of an old entry precedes, in this wavefront's LDS order, the write reusing it)
         sh.vbuf()[v] = 0.f;
-        rinv_ok = false;  // R^-1 is not updated through a drop: back substitution from here on
         const int k = __builtin_amdgcn_readfirstlane(kk);
         const int ak = rli(act_reg, k);
         if (v == 0) sh.cmask[ak / 6] &= (unsigned char)~(1u << (ak % 6));
@@ -749,6 +748,29 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           }
           if (v == 0) *reinterpret_cast<float2*>(&sh.u.gi.cs[2 * j]) = make_float2(cc, sn);
           lsync();
+        }
+        // R^-1 through the drop. With H = R E (column k removed) and R' = G' H restricted to its
+        // first q - 1 rows (the Givens chain above), E' R^-1 is a left inverse of H, so
+        //   R'^-1 = E' R^-1 G[:, 0:q-1]:
+        // R^-1 without row k, the same rotations on its columns as on J's (j = k .. q-2), the
+        // last column dropped. Lane i streams its row through the chain with one carried value
+        // (rows i > k move up one; their entries left of column i - 1 are zero and stay so).
+        if (rinv_ok) {
+          using S = SharedC1<NV>;
+          const int i = v;
+          const bool live = i < q && i != k;
+          const int i2 = (i > k) ? i - 1 : i;
+          int j = (i > k) ? i - 1 : k;  // first rotation that touches row i
+          float carry = (live && j >= i) ? sh.P[S::RB + rcol(j) + i] : 0.f;
+          for (int jj = k; jj <= q - 2; jj++) {
+            const float2 cs2 = *reinterpret_cast<const float2*>(&sh.u.gi.cs[2 * jj]);
+            const float b = (live && jj >= j && jj + 1 >= i) ? sh.P[S::RB + rcol(jj + 1) + i] : 0.f;
+            lsync();
+            if (live && jj >= j) {
+              sh.P[S::RB + rcol(jj) + i2] = fmaf(cs2.x, carry, cs2.y * b);
+              carry = fmaf(-cs2.y, carry, cs2.x * b);
+            }
+          }
         }
       }
       lsync();

@@ -539,7 +539,7 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
   }
 }
 
-template <int NV>
+template <int NV, bool REFINE>
 __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KParams& P,
                                         SharedW<NV>& sh, float* __restrict__ fout,
                                         uint8_t* __restrict__ st_out, int32_t* __restrict__ it_out) {
@@ -926,8 +926,10 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
   int p = -1;
   Cons cp{};
   float up = 0.f;
+  int it_refined = -1;  // active-set trips at the last refinement
+  int passes = 0;       // refinements so far
   if (status == CMPC_OK && CMPC_DIAG_STOP == 0) {
-   for (int pass = 0;; pass++) {
+   for (;;) {
     for (;;) {
       wpin(slot);
       CMPC_WIDE_IDS();
@@ -957,7 +959,10 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         }
         const float xmax = wave_max(xm);
         wave_argmin(best, bid);
-        const float tol = 1e-5f * fmaxf(1.f, xmax);
+        // after a refinement x is the exact QP's optimum on the working set up to fp32 rounding:
+        // the constraints are held to that (a face the fp32 solve left for a nearly active
+        // constraint shows here as a violation of ~1e-6 x_max, and joins the working set)
+        const float tol = (passes ? 2e-7f : 1e-5f) * fmaxf(1.f, xmax);
         if (bid == kNoneW || best >= -tol) break;
         p = __builtin_amdgcn_readfirstlane(bid);
         cp = decode_cons(p, mui, sh.sub[p / 6]);
@@ -1160,7 +1165,6 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         // re-triangularise rows kk..q-1 with Givens rotations (wave 0, in place)
         const int k = kk;
         seam = (q > NH);
-        rinv_ok = false;  // R^-1 is not updated through a drop: back substitution from here on
         if (t < NV) {
           sh.vbuf()[lidx<NV>(t)] = 0.f;
           if (t < k || t > q - 2)
@@ -1237,6 +1241,29 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
               *reinterpret_cast<float2*>(&sh.cs()[2 * j + (j >= NH ? 4 : 0)]) = make_float2(cc, sn);
             wlsync();
           }
+          // R^-1 through the drop: R'^-1 = E' R^-1 G[:, 0:q-1] (row k removed, the rotations of
+          // the chain above applied to its columns as to J's, the last column dropped; class 1
+          // derives it). Lane row i = lane + 64 m streams through the chain with one carried value
+          if (rinv_ok) {
+#pragma unroll
+            for (int m = 0; m < RQ; m++) {
+              const int i = lane + 64 * m;
+              const bool live = i < q && i != k;
+              const int i2 = (i > k) ? i - 1 : i;
+              const int j0 = (i > k) ? i - 1 : k;  // first rotation that touches row i
+              float carry = (live && j0 >= i) ? sh.P[G::O_RINV + rcol_w(j0) + i] : 0.f;
+              for (int jj = k; jj <= q - 2; jj++) {
+                const float2 cs2 = *reinterpret_cast<const float2*>(&sh.cs()[2 * jj + (jj >= NH ? 4 : 0)]);
+                const float b = (live && jj >= j0) ? sh.P[G::O_RINV + rcol_w(jj + 1) + i] : 0.f;
+                wlsync();
+                if (live && jj >= j0) {
+                  sh.P[G::O_RINV + rcol_w(jj) + i2] = fmaf(cs2.x, carry, cs2.y * b);
+                  carry = fmaf(-cs2.y, carry, cs2.x * b);
+                }
+              }
+              wlsync();
+            }
+          }
         }
       }
       wbar();
@@ -1308,10 +1335,16 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         q--;
       }
     }
-    // converged: one refinement step (from N = 11), then the constraints are checked again (a
-    // step that violates one continues the dual active set from the refined point)
-    if (pass > 0 || !(CMPC_WIDE_REFINE && P.refine) || status != CMPC_OK) break;
+    // converged: a refinement step (from N = 11), then the constraints are checked again (to
+    // the refined tolerance above). A step that violates one continues the dual active set from
+    // the refined point, whose new steps are fp32 again: the new face is refined in turn (at most
+    // four refinements; none when the working set did not move since the last one)
+    if (passes >= 4 || (passes > 0 && iters == it_refined) || !(REFINE && P.refine) ||
+        status != CMPC_OK)
+      break;
     rinv_ok = false;  // the R^-1 area is the refinement's scratch from here on
+    it_refined = iters;
+    passes++;
     wide_refine<NV>(rec, P, sh, slot, xv, q, n, wave);
    }
   }
@@ -1370,7 +1403,9 @@ struct WideArgs {
   KParams P;
 };
 
-template <int NV, bool PERSIST>
+// REFINE is part of the kernel's name: the refining and plain builds of a class live in different
+// units, and one instantiation name would let the linker keep only one of them
+template <int NV, bool PERSIST, bool REFINE>
 __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGPR_ATTR void cmpc_solve_w_kernel(
     WideArgs A) {
   __shared__ SharedW<NV> sh;
@@ -1379,8 +1414,8 @@ __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGP
     const int b = blockIdx.x;
     if (b >= count) return;
     const int inst = A.in_list[b];
-    solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
-                A.status + inst, A.iters ? A.iters + inst : nullptr);
+    solve_w<NV, REFINE>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
+                        A.status + inst, A.iters ? A.iters + inst : nullptr);
   } else {
     for (int round = 0;; round++) {
       // deq == nullptr (single-instance path): workgroup i takes entry i, once
@@ -1389,18 +1424,18 @@ __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGP
       const int b = __builtin_amdgcn_readfirstlane(sh.deq_b);
       if (b >= count) break;
       const int inst = A.in_list[b];
-      solve_w<NV>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
-                  A.status + inst, A.iters ? A.iters + inst : nullptr);
+      solve_w<NV, REFINE>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
+                          A.status + inst, A.iters ? A.iters + inst : nullptr);
       wbar();  // every wave is done with this instance's LDS before the next record lands there
     }
   }
 }
 
-template <int NV, bool PERSIST>
+template <int NV, bool PERSIST, bool REFINE>
 int wide_grid_cap() {
   static const int cap = [] {
     int nb = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc_solve_w_kernel<NV, PERSIST>, WGeo<NV>::NT,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc_solve_w_kernel<NV, PERSIST, REFINE>, WGeo<NV>::NT,
                                                      0) != hipSuccess ||
         nb <= 0)
       nb = 1;
@@ -1427,12 +1462,15 @@ hipError_t launch_wide_impl(const float* d_recs, const KParams& P, float* d_forc
   WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, in_count, persist ? deq : nullptr, P};
   if (persist) {
     if constexpr (kPersist) {
-      if (deq) grid = grid < wide_grid_cap<NV, true>() ? grid : wide_grid_cap<NV, true>();
-      hipLaunchKernelGGL((cmpc_solve_w_kernel<NV, true>), dim3(grid), dim3(WGeo<NV>::NT), 0, stream, A);
+      constexpr bool kRef = CMPC_WIDE_REFINE != 0;
+      if (deq) grid = grid < wide_grid_cap<NV, true, kRef>() ? grid : wide_grid_cap<NV, true, kRef>();
+      hipLaunchKernelGGL((cmpc_solve_w_kernel<NV, true, CMPC_WIDE_REFINE != 0>), dim3(grid), dim3(WGeo<NV>::NT), 0,
+                         stream, A);
     }
   } else {
     if constexpr (kOne)
-      hipLaunchKernelGGL((cmpc_solve_w_kernel<NV, false>), dim3(grid), dim3(WGeo<NV>::NT), 0, stream, A);
+      hipLaunchKernelGGL((cmpc_solve_w_kernel<NV, false, CMPC_WIDE_REFINE != 0>), dim3(grid), dim3(WGeo<NV>::NT), 0,
+                         stream, A);
   }
   return hipGetLastError();
 }

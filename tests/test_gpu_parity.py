@@ -54,8 +54,12 @@ def assert_parity(orc, recs, prm, f, q_ref, ok=None, label=""):
             sc = max(np.abs(x64).max(), 1.0)
             e64s.append(np.abs(f[i] - x64).max() / sc)
             eref.append(np.abs(q_ok[b] - x64).max() / sc)
+        gait = recs[idx, 32 + 12 * prm.horizon:32 + 13 * prm.horizon].copy().view(np.uint8)
+        n_bad = 3 * (gait != 0).sum(1)
         print(msg + f" -> fp64-optimum branch: worst vs qpOASES {err[bad].max():.2e}, ours vs the "
-              f"fp64 optimum <= {max(e64s):.2e}, the reference's {min(eref):.2e}..{max(eref):.2e}")
+              f"fp64 optimum <= {max(e64s):.2e}, the reference's {min(eref):.2e}..{max(eref):.2e}; "
+              f"reduced sizes n {sorted(set(n_bad.tolist()))}, ours vs fp64 per instance "
+              f"{[f'{e:.1e}' for e in e64s[:8]]}")
         assert max(e64s) <= FP64_BRANCH_TOL, (err.max(), max(e64s))
         return
     print(msg)
