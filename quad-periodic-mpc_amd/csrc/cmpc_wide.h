@@ -54,6 +54,14 @@
 #ifndef CMPC_WIDE_REFINE
 #define CMPC_WIDE_REFINE 1
 #endif
+// refinements per instance at most, and the constraint tolerance (x x_max) after one
+#ifndef CMPC_REFINE_MAX
+#define CMPC_REFINE_MAX 4
+#endif
+#ifndef CMPC_REFINE_TOL
+#define CMPC_REFINE_TOL 2e-7f
+#endif
+
 
 namespace cmpc {
 namespace {
@@ -259,17 +267,18 @@ __device__ __forceinline__ int rli_pos(const int (&a)[RQ], int i) {
 //      within a wave and over the waves in order through the LDS: deterministic) and x -= J2 u.
 // The reference's own fp32 pipeline (dense-S GEMMs) is up to ~1e-4 from its QP's exact optimum at
 // N >= 16; after this step the solution lands within ~1e-6 of it.
+// Phases A-D of wide_refine: the exact QP's gradient at x (xs[] in LDS) into the refinement
+// scratch (24 + 12 N doubles in the R^-1 area). (Out of line, the call saved 95 VGPRs of the J
+// rows around it: N = 16 10.0 -> 8.8 M QP/s, abr2.)
 template <int NV>
-__device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, const KParams& P, SharedW<NV>& sh,
-                                            float (&slot)[WGeo<NV>::NH], float& xv, int q, int n, int wave) {
+__device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in, const KParams& P,
+                                                     SharedW<NV>& sh, int wave) {
   using G = WGeo<NV>;
-  constexpr int NH = G::NH;
-  constexpr int NC = (NH + 63) / 64;
   constexpr int S0 = 24;  // [0..8] R, [9..17] I_w^-1, [18] x_drag, [19] f_est term, [20] x0[12], [21..23] rpy
-  // This runs inside the active-set loop: an opaque record pointer keeps its loads (and the
-  // arithmetic on them) from being hoisted out of the loop and kept live across every trip. The
-  // fp64 scalars come from the kernel arguments (SGPRs) or the LDS, never long-lived VGPRs: the
-  // 96-column class has 48 VGPRs beside its J row.
+  // an opaque record pointer keeps its loads (and the arithmetic on them) from being hoisted out
+  // of the active-set loop and kept live across every trip. The fp64 scalars come from the kernel
+  // arguments (SGPRs) or the LDS, never long-lived VGPRs: the 96-column class has 48 VGPRs beside
+  // its J row
   const float* rec = rec_in;
   asm volatile("" : "+s"(rec));
   double* scr = reinterpret_cast<double*>(&sh.P[G::O_RINV]);
@@ -408,34 +417,34 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
     // forward: z_j += (N1 z)_j + d_k,j   (N1 = Adt - I: rows 0..2 dt R' z[6:9], 3, 4 dt z9, z10,
     // 5 dt z11 + dt^2/2 x_drag z9, 11 dt x_drag z9; z12 = 0)
     double z = 0.0;
+    // per-lane coefficients of (z6 .. z11): one branch-free FMA chain per step (per-lane branches
+    // measured 5 % slower at N = 16, 3.5 % at config 5: same-box A/B abr1)
+    double c6 = 0.0, c7 = 0.0, c8 = 0.0, c9 = 0.0, c10 = 0.0, c11 = 0.0;
+    if (jj < 3) { c6 = dt * R[jj]; c7 = dt * R[3 + jj]; c8 = dt * R[6 + jj]; }
+    if (jj == 3) c9 = dt;
+    if (jj == 4) c10 = dt;
+    if (jj == 5) { c11 = dt; c9 = dth * scr[18]; }
+    if (jj == 11) c9 = dt * scr[18];
     for (int k = 0; k < N; k++) {
       const double dk = scr[S0 + 12 * k + jj];
       const double z6 = rl_d(z, 6), z7 = rl_d(z, 7), z8 = rl_d(z, 8);
       const double z9 = rl_d(z, 9), z10 = rl_d(z, 10), z11 = rl_d(z, 11);
-      double nz;
-      if (jj < 3) nz = dt * (R[jj] * z6 + R[3 + jj] * z7 + R[6 + jj] * z8);
-      else if (jj == 3) nz = dt * z9;
-      else if (jj == 4) nz = dt * z10;
-      else if (jj == 5) nz = dt * z11 + dth * scr[18] * z9;
-      else if (jj == 11) nz = dt * scr[18] * z9;
-      else nz = 0.0;
-      z += nz + dk;
+      z += c6 * z6 + c7 * z7 + c8 * z8 + c9 * z9 + c10 * z10 + c11 * z11 + dk;
       if (j < 12) scr[S0 + 12 * k + j] = (double)wf * z;  // S e_k
     }
     // backward: mu_j += (N1' mu)_j + S e_k,j  (rows 6..8 dt R mu[0:3], 9 dt (mu3 + x_drag mu11) +
     // dt^2/2 x_drag mu5, 10 dt mu4, 11 dt mu5)
     double mu = 0.0;
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0, e4 = 0.0, e5 = 0.0, e11 = 0.0;
+    if (jj >= 6 && jj < 9) { e0 = dt * R[3 * (jj - 6)]; e1 = dt * R[3 * (jj - 6) + 1]; e2 = dt * R[3 * (jj - 6) + 2]; }
+    if (jj == 9) { e3 = dt; e11 = dt * scr[18]; e5 = dth * scr[18]; }
+    if (jj == 10) e4 = dt;
+    if (jj == 11) e5 = dt;
     for (int k = N - 1; k >= 0; k--) {
       const double sk = scr[S0 + 12 * k + jj];
       const double m0 = rl_d(mu, 0), m1 = rl_d(mu, 1), m2 = rl_d(mu, 2), m3 = rl_d(mu, 3);
       const double m4 = rl_d(mu, 4), m5 = rl_d(mu, 5), m11 = rl_d(mu, 11);
-      double nm;
-      if (jj >= 6 && jj < 9) nm = dt * (R[3 * (jj - 6)] * m0 + R[3 * (jj - 6) + 1] * m1 + R[3 * (jj - 6) + 2] * m2);
-      else if (jj == 9) nm = dt * (m3 + scr[18] * m11) + dth * scr[18] * m5;
-      else if (jj == 10) nm = dt * m4;
-      else if (jj == 11) nm = dt * m5;
-      else nm = 0.0;
-      mu += nm + sk;
+      mu += e0 * m0 + e1 * m1 + e2 * m2 + e3 * m3 + e4 * m4 + e5 * m5 + e11 * m11 + sk;
       if (j < 12) scr[S0 + 12 * k + j] = mu;
     }
   }
@@ -468,6 +477,19 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
     if (t < 6 * N) scr[S0 + 12 * (t / 6) + t - 6 * (t / 6)] = ev;
   }
   wbar();
+}
+
+template <int NV>
+__device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, const KParams& P, SharedW<NV>& sh,
+                                            float (&slot)[WGeo<NV>::NH], float& xv, int q, int n, int wave) {
+  using G = WGeo<NV>;
+  constexpr int NH = G::NH;
+  constexpr int NC = (NH + 63) / 64;
+  constexpr int S0 = 24;  // [0..8] R, [9..17] I_w^-1, [18] x_drag, [19] f_est term, [20] x0[12], [21..23] rpy
+  const float* rec = rec_in;
+  asm volatile("" : "+s"(rec));
+  double* scr = reinterpret_cast<double*>(&sh.P[G::O_RINV]);
+  refine_residual<NV>(rec, P, sh, wave);
   // ---- E: row r's gradient entry, u = J2' r, x -= J2 u
   float rr = 0.f;
   {
@@ -485,7 +507,6 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
   float pa[NC], pb[NC];
 #pragma unroll
   for (int m = 0; m < NC; m++) { pa[m] = 0.f; pb[m] = 0.f; }
-#ifndef CMPC_RB_NODPP
   {
     const int ln = lane_opq();
     static_for<0, NH>([&](auto JC) {
@@ -523,7 +544,6 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
       wbar();
     }
   }
-#endif
   {
     CMPC_WIDE_IDS();
     f2v acc = {0.f, 0.f};
@@ -962,7 +982,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         // after a refinement x is the exact QP's optimum on the working set up to fp32 rounding:
         // the constraints are held to that (a face the fp32 solve left for a nearly active
         // constraint shows here as a violation of ~1e-6 x_max, and joins the working set)
-        const float tol = (passes ? 2e-7f : 1e-5f) * fmaxf(1.f, xmax);
+        const float tol = (passes ? CMPC_REFINE_TOL : 1e-5f) * fmaxf(1.f, xmax);
         if (bid == kNoneW || best >= -tol) break;
         p = __builtin_amdgcn_readfirstlane(bid);
         cp = decode_cons(p, mui, sh.sub[p / 6]);
@@ -1339,7 +1359,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     // the refined tolerance above). A step that violates one continues the dual active set from
     // the refined point, whose new steps are fp32 again: the new face is refined in turn (at most
     // four refinements; none when the working set did not move since the last one)
-    if (passes >= 4 || (passes > 0 && iters == it_refined) || !(REFINE && P.refine) ||
+    if (passes >= CMPC_REFINE_MAX || (passes > 0 && iters == it_refined) || !(REFINE && P.refine) ||
         status != CMPC_OK)
       break;
     rinv_ok = false;  // the R^-1 area is the refinement's scratch from here on
