@@ -151,7 +151,7 @@ def _config5_state(cm, R, recs_np, B):
 
 def load_pmc(N: int, batch: int, kernel_prefix: str):
     """HBM bytes per launch of the dominant kernel + its SQ counters from the committed
-    rocprofv3 PMC summary (profiles/pmc_summary.json, scripts/pmc_summary.py)."""
+    rocprofv3 PMC summary (profiles/pmc_summary.json, scripts/pmc_collect.py)."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as f:
             d = json.load(f)

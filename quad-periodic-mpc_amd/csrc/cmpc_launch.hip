@@ -173,9 +173,14 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], dq(1, 81, 96),
                                            grid_of[1], ctx.side[1])) != hipSuccess)
       return e;
-    // side 0: the 120-column build (every trot instance at N = 20); side 1: 121..128 and 144
+    // the 120-column build on side 0 from N = 14 (every trot instance at N = 17..20, beside the
+    // 96-column trot class at N = 14..16); below, on side 1 behind the sparse 96 class: at N = 10
+    // its launch (few or no instances) otherwise lengthens side 0's 80-class chain, the step's
+    // critical path (config 3 timeline, profiles/r04_prof). CMPC_W120_SIDE=0/1 forces a side (A/B)
+    static const int w120_env = diag_knob("CMPC_W120_SIDE", -1);
+    const int w120_side = (w120_env >= 0) ? (w120_env & 1) : (6 * P.N <= 80 ? 1 : 0);
     if (n_max > 96 && (e = launch_wide_w120(d_recs, P, d_forces, d_status, d_iters, list[8], &cnt[9],
-                                            dq(8, 97, 120), grid_of[8], ctx.side[0])) != hipSuccess)
+                                            dq(8, 97, 120), grid_of[8], ctx.side[w120_side])) != hipSuccess)
       return e;
     if (n_max > 120 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
                                              dq(2, 121, 128), grid_of[2], ctx.side[1])) != hipSuccess)

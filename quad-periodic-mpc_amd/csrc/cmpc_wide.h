@@ -55,6 +55,9 @@
 #define CMPC_WIDE_REFINE 1
 #endif
 // refinements per instance at most, and the constraint tolerance (x x_max) after one
+#ifndef CMPC_DIAG_REF_SKIP  // diagnostic builds: skip refinement phases (bit 0..4 = A..E; wrong results)
+#define CMPC_DIAG_REF_SKIP 0
+#endif
 #ifndef CMPC_REFINE_MAX
 #define CMPC_REFINE_MAX 4
 #endif
@@ -112,11 +115,12 @@ struct WGeo {
   static constexpr int O_DFULL = O_BUFB + VL, O_XS = O_DFULL + NV, O_CS = O_XS + NV;
   static constexpr int GI_END = O_CS + 2 * NV + 8;
   // R^-1 beside R for the first QI active-set positions (sized to keep each class's workgroups
-  // per CU: 80 / 96 six, 120 / 128 four)
+  // per CU: 80 / 96 six, 120 / 128 four; at 80 the LDS it does not take lets class 1's one-wave
+  // workgroups share the CU: QI 56 -> 36 config 3 +1.7 %, profiles/r04_ab/r04_ab80q2)
 #ifdef CMPC_WIDE_QI
   static constexpr int QI = CMPC_WIDE_QI;
 #else
-  static constexpr int QI = (NV == 80) ? 56 : (NV == 96) ? 40 : (NV == 120) ? 48 : (NV == 128) ? 32
+  static constexpr int QI = (NV == 80) ? 36 : (NV == 96) ? 40 : (NV == 120) ? 48 : (NV == 128) ? 32
                             : (NV == 144) ? 40 : 64;
 #endif
   static constexpr int O_RINV = (GI_END + 3) & ~3;
@@ -286,7 +290,7 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
   const double dt = P.dt64, dth = P.dth64, dt3 = P.dt3_64;
   const float* xs = sh.xs();
   // ---- A: per step and axis, sum_b r_b x u_b and sum_b u_b; R, I_w^-1 and the instance scalars
-  {
+  if (!(CMPC_DIAG_REF_SKIP & 1)) {
     const int t = 64 * wave + lane_opq();
     if (t < 3 * N) {
       const int k = t / 3, a = t - 3 * (t / 3);
@@ -347,7 +351,7 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
   }
   wbar();
   // ---- B: d_k,j = (Bdt u_k + Qdt f)_j + (Adt X_d,k-1)_j - X_d,k,j  (X_d,-1 = x0; component 12 = g)
-  {
+  if (!(CMPC_DIAG_REF_SKIP & 2)) {
     const double* R = scr;
     const double* Ii = scr + 9;
     const float* traj = rec + CMPC_REC_HDR;
@@ -407,7 +411,7 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
   wbar();
   // ---- C: wave 0, lane j < 12 owns component j of z, then of mu. Each step's coefficients are
   // re-read from the LDS (R) and the kernel arguments: nothing but z / mu stays live
-  if (wave == 0) {
+  if (wave == 0 && !(CMPC_DIAG_REF_SKIP & 4)) {
     const int j = lane_opq();
     const int jj = (j < 12) ? j : 11;
     const double* R = scr;
@@ -450,7 +454,7 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
   }
   wbar();
   // ---- D: per step, y_k = I_w^-1 nu_k[6:9] and nu_k[9:12] / m into the step's first 6 slots
-  {
+  if (!(CMPC_DIAG_REF_SKIP & 8)) {
     const int t = 64 * wave + lane_opq();
     double ev = 0.0;
     if (t < 6 * N) {
@@ -485,7 +489,6 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
   using G = WGeo<NV>;
   constexpr int NH = G::NH;
   constexpr int NC = (NH + 63) / 64;
-  constexpr int S0 = 24;  // [0..8] R, [9..17] I_w^-1, [18] x_drag, [19] f_est term, [20] x0[12], [21..23] rpy
   const float* rec = rec_in;
   asm volatile("" : "+s"(rec));
   double* scr = reinterpret_cast<double*>(&sh.P[G::O_RINV]);
@@ -507,7 +510,7 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
   float pa[NC], pb[NC];
 #pragma unroll
   for (int m = 0; m < NC; m++) { pa[m] = 0.f; pb[m] = 0.f; }
-  {
+  if (!(CMPC_DIAG_REF_SKIP & 16)) {
     const int ln = lane_opq();
     static_for<0, NH>([&](auto JC) {
       constexpr int j = decltype(JC)::value;
@@ -555,7 +558,7 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
       CMPC_WSWEEP_FENCE(j);
     }
     const float dx = pair_sum(acc.x + acc.y);
-    if (r < n) xv -= dx;
+    if (r < n && !(CMPC_DIAG_REF_SKIP & 16)) xv -= dx;
   }
 }
 
