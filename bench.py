@@ -270,8 +270,10 @@ def local_leg(args, cm, prm, config, N, B, steps, warmup, dev, rank, barrier, sy
         est.copy_(est0)
         t_next[0] = 10.4
     sync()
-    if solver is not None:
-        solver.enable_timing(steps)
+    if solver is not None and os.environ.get("CMPC_BENCH_NO_EVENTS") != "1":  # diagnostic: events off
+        # HIP events on every TIMING_EVERY-th solve of the timed loop: each recorded solve adds
+        # event packets between its launches (on every solve they cost config 3 1.9 %, r04_ev3)
+        solver.enable_timing((steps + TIMING_EVERY - 1) // TIMING_EVERY, every=TIMING_EVERY)
     # ---- timed region: K steps, bracketed by barrier + synchronize on both sides ----------
     barrier()
     sync()
@@ -289,6 +291,7 @@ def local_leg(args, cm, prm, config, N, B, steps, warmup, dev, rank, barrier, sy
                 recs=recs, recs_np=recs_np, world=world)
 
 
+TIMING_EVERY = 4   # the solves of a timed loop that record the roofline's HIP events
 WIDE_CLASS_NV = (80, 96, 120, 128, 144, 192, 256)   # row widths of the wide classes (cmpc_wide.h)
 
 
@@ -335,6 +338,7 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
         "units_per_launch": int(units1),
         "flops_per_unit": fl,
         "avg_launch_ms": round(t1 * 1e3, 4),
+        "launches_timed": int(launch_ms.shape[0]),
         "class1_avg_launch_ms": round(float(np.mean(c1)), 4),
         "tail_avg_ms": round(float(np.mean(c2)), 4),
         "wide_class_units": int(ovf),
@@ -342,7 +346,8 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
         "hbm_gbs": round(algorithmic_bytes(N, config == 5) * value / 1e9, 3),
         "note": "FP32 VALU roof (the path is latency/VALU-bound, not HBM: ~1300 FLOP/B). "
                 "achieved = SURVEY §8(d) F(N) (dense reference algorithm) x instances of "
-                "the launch / its HIP-event time on the solver stream; the kernels execute "
+                "the launch / its HIP-event time on the solver stream (events on every "
+                f"{TIMING_EVERY}th solve of the timed loop, `launches_timed` of them); the kernels execute "
                 "fewer flops (reduced n, structured condensation), so frac is speed against "
                 "the reference's work. valu_pmc: counters of the same kernel (profiles/"
                 "pmc_summary.json); valu_issue_util = VALU instructions x 2 cycles (wave64 on "

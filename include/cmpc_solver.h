@@ -282,6 +282,9 @@ CMPC_EXTERNC int cmpc_batch_rollout(cmpc_batch* h, float* d_loco, const float* d
  * have joined] and the number of instances the last solve listed for the wide classes
  * (n > 64). Synchronises. */
 CMPC_EXTERNC int cmpc_batch_enable_timing(cmpc_batch* h, int steps);
+/* The same on every `every`-th solve only (the first of each group of `every`), `steps` of them:
+ * a timed loop then pays the event packets on a fraction of its solves. */
+CMPC_EXTERNC int cmpc_batch_enable_timing_every(cmpc_batch* h, int steps, int every);
 CMPC_EXTERNC int cmpc_batch_read_timing(cmpc_batch* h, float* ms, int* steps_recorded,
                                         int* class1_overflow);
 /* Stream the handle runs on (hipStream_t). */

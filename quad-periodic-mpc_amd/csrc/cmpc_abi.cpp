@@ -57,7 +57,12 @@ struct cmpc_batch {
   // optional per-launch timing (cmpc_batch_enable_timing)
   std::vector<hipEvent_t> ev;
   int ev_steps = 0, ev_next = 0;
+  int ev_every = 1, ev_solves = 0;  // events on every ev_every-th solve (cmpc_batch_enable_timing_every)
 };
+
+#ifndef CMPC_REFINE_FROM_N
+#define CMPC_REFINE_FROM_N 11  // first horizon whose wide classes refine (diagnostic builds move it)
+#endif
 
 static cmpc::KParams make_kparams(const cmpc_params& p) {
   cmpc::KParams k{};
@@ -71,7 +76,7 @@ static cmpc::KParams make_kparams(const cmpc_params& p) {
   k.max_iter = p.max_iter > 0 ? p.max_iter : 100;
   // the fp32 pipelines of the reference and of this solver are within ~1e-5 of the exact optimum
   // at N <= 10 and drift to ~1e-4 beyond: the refinement runs from N = 11
-  k.refine = p.horizon > 10 ? 1 : 0;
+  k.refine = p.horizon >= CMPC_REFINE_FROM_N ? 1 : 0;
   k.dt64 = (double)k.dt;
   k.dth64 = 0.5 * k.dt64 * k.dt64;
   k.dt3_64 = k.dt64 * k.dt64 * k.dt64 / 6.0;
@@ -202,9 +207,13 @@ extern "C" int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int batch
     return -1;
   }
   hipEvent_t* ev = nullptr;
-  if (h->ev_steps > 0 && h->ev_next < h->ev_steps) ev = &h->ev[3 * h->ev_next++];
-  hipError_t e = cmpc::launch_solve(d_records, batch, h->kp, d_forces, d_status, d_iters, h->d_work,
-                                    h->max_batch, h->stream, h->ctx, ev);
+  if (h->ev_steps > 0 && h->ev_next < h->ev_steps && h->ev_solves++ % h->ev_every == 0)
+    ev = &h->ev[3 * h->ev_next++];
+  // (A HIP graph of this launch sequence, replayed while the arguments repeat, measured config 3
+  // 41.8 M -> 32.5 M and config 2 14.7 M -> 9.8 M QP/s: the replay lost the overlap of class 1
+  // with the side-stream classes, profiles/r04_ab/r04_m*. Direct launches only.)
+  const hipError_t e = cmpc::launch_solve(d_records, batch, h->kp, d_forces, d_status, d_iters, h->d_work,
+                                          h->max_batch, h->stream, h->ctx, ev);
   if (e != hipSuccess) return fail("launch_solve", e);
   return 0;
 }
@@ -254,7 +263,13 @@ extern "C" int cmpc_batch_rollout(cmpc_batch* h, float* d_loco, const float* d_r
 }
 
 extern "C" int cmpc_batch_enable_timing(cmpc_batch* h, int steps) {
-  if (!h || steps < 0) return -1;
+  return cmpc_batch_enable_timing_every(h, steps, 1);
+}
+
+extern "C" int cmpc_batch_enable_timing_every(cmpc_batch* h, int steps, int every) {
+  if (!h || steps < 0 || every < 1) return -1;
+  h->ev_every = every;
+  h->ev_solves = 0;
   for (auto e : h->ev) (void)hipEventDestroy(e);
   h->ev.assign(3 * (size_t)steps, nullptr);
   for (auto& e : h->ev)

@@ -57,6 +57,7 @@ struct LocoParams {
 constexpr int kLists = 9;
 constexpr int kHdr = 32;
 constexpr int kDeq = 16;  // cnt[kDeq + list]: dequeue counter of a persistent class's workgroups
+static_assert(1 + kLists <= kDeq && kDeq + kLists <= kHdr, "list lengths and dequeue counters fit the header");
 inline size_t work_ints(int max_batch) { return kHdr + kLists * (size_t)max_batch; }
 // Side streams and events of one handle: the wider size classes run concurrently with class 1
 // (they are latency-bound: few instances, long serial solves). Two side streams: with the

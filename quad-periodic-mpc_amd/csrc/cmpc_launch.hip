@@ -67,34 +67,16 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
 // (the same threshold as class 1's split) the drains are short and every class is one-per-entry
 // (config 2: 11.3 M -> 11.7 M QP/s).
 // CMPC_WIDE_FORM (A/B): 1 every class one-per-entry, 2 every class persistent.
-// the one-workgroup-per-entry launch form only for the class that holds 6 N itself (1), or for
-// every class meeting 6 N +- 3 sqrt(N) (0, round 3)
-#ifndef CMPC_POPULOUS_EXACT
-#define CMPC_POPULOUS_EXACT 0
-#endif
+// (Only the class holding 6 N itself one-per-entry measured -0.3 % at config 3, round 4.)
 bool one_per_entry(int lo, int hi, int N, int batch) {
   static const int form = diag_knob("CMPC_WIDE_FORM", 0);
   if (form == 1 || batch < 16384) return true;
   if (form == 2) return false;
-#if CMPC_POPULOUS_EXACT
-  return lo <= 6 * N && 6 * N <= hi;  // only the class holding the trot size itself
-#else
   const float mode = 6.f * (float)N, half = 3.f * sqrtf((float)N);
   return (float)hi >= mode - half && (float)lo <= mode + half;
-#endif
 }
 
 }  // namespace
-
-// Grid of the 80-column class when it is launched ahead of class 1 (0: off). At N <= 10 class 1
-// holds the trot size and carries the batch; its one-wave workgroups take every wave slot a CU
-// frees, so the three-wave 80-column workgroups of the random-contact instances were dispatched
-// late and ended 0.3 ms after class 1 (round-3 kernel trace). Ahead: classify first on the
-// handle's stream, then a persistent 80-column grid of this many workgroups (resident before class
-// 1 starts) dequeues that class's list while class 1 fills the rest of the GPU.
-#ifndef CMPC_WIDE_AHEAD
-#define CMPC_WIDE_AHEAD 0
-#endif
 
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
@@ -123,10 +105,9 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // kernels (profiles/r03_ab/sweep2): beside class 1 +2 % at 16384 .. 131072 instances, within
     // noise below. CMPC_CLASSIFY_SIDE=0/1 forces either placement (A/B).
     static const int cls_env = diag_knob("CMPC_CLASSIFY_SIDE", -1);
-    // the 80-column class ahead of class 1 (CMPC_WIDE_AHEAD): large batches whose class 1 holds
-    // the trot size (6 N <= 60)
-    const bool ahead = CMPC_WIDE_AHEAD > 0 && batch >= 16384 && 6 * P.N <= 60;
-    const bool cls_side = ahead ? false : (cls_env < 0) ? (batch >= 16384) : (cls_env == 1);
+    // (Round 4 also measured the 80-column class launched ahead of class 1 as a persistent grid
+    // resident before class 1 starts: config 3 -1 to -3 %, dropped.)
+    const bool cls_side = (cls_env < 0) ? (batch >= 16384) : (cls_env == 1);
     hipStream_t cs = cls_side ? ctx.side[0] : stream;
     if (cls_side) {
       if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
@@ -167,7 +148,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // side 0: 80, 120, 144, 256; side 1: 96, 128, 192 (at N = 20 the 120-column class, which
     // carries the batch, runs beside the 128-column class)
     if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1],
-                             ahead ? &cnt[kDeq + 0] : dq(0, 65, 80), ahead ? CMPC_WIDE_AHEAD : grid_of[0],
+                             dq(0, 65, 80), grid_of[0],
                              ctx.side[0])) != hipSuccess)
       return e;
     if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], dq(1, 81, 96),
@@ -228,8 +209,11 @@ hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_f
   if (n <= 64)
     return launch_class1(n <= 60 ? 60 : 64, d_rec, 1, P, d_forces, d_status, d_iters, nullptr,
                          nullptr, nullptr, nullptr, 1, stream);
-  // the same kernel binary as the batched launch would use for this class (the two launch forms
-  // may round differently): the persistent form runs its loop once with deq == nullptr
+  // the launch form the batched launch of this class would pick for a batch of one (one workgroup
+  // per entry; the persistent form runs its loop once with deq == nullptr). Both forms round
+  // alike (-ffp-contract=on, build.py): tests/test_gpu_parity.py::test_batch_size_invariance
+  // solves the same records in a batch of 16384 (persistent sparse classes), in batches of 4096
+  // and one at a time and requires bitwise-equal forces
 #define CMPC_SINGLE_WIDE(W, LO, HI)                                                                 \
   if (n <= HI)                                                                                      \
     return one_per_entry(LO, HI, P.N, 1)                                                            \

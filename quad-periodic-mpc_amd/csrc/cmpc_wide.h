@@ -153,7 +153,7 @@ struct SharedW {
   int sfs[4 * MAXN];          // stance foot-step ids, in order
   int blkbase[MAXN + 2];      // first reduced variable of each horizon step
   unsigned char varblk[G::NT], varcol[G::NT];
-  unsigned char stance[4 * MAXN];
+  alignas(4) unsigned char stance[4 * MAXN];
   unsigned char cflag[2 * NV + 8];  // active flag per constraint id (6 per stance foot-step)
   int deq_b;                  // list entry dequeued by the workgroup (persistent launches)
   __device__ __forceinline__ float (*BdtT())[16] { return reinterpret_cast<float(*)[16]>(&P[G::PSZ]); }
@@ -296,15 +296,40 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
       const int k = t / 3, a = t - 3 * (t / 3);
       const int a1 = (a == 2) ? 0 : a + 1, a2 = (a == 0) ? 2 : a - 1;
       double tc = 0.0, sc = 0.0;
-      int v = sh.blkbase[k];
+      if constexpr (NV <= 96) {
+        // branch-free over the feet: the lever arms (one global round trip for all eight) and the
+        // step's four stance bytes (one LDS word) first, so every x read's address is known up front
+        // (per-lane stance branches had serialised a load round trip per foot)
+        float ra1[4], ra2[4];
 #pragma unroll
-      for (int f = 0; f < 4; f++) {
-        if (sh.stance[4 * k + f]) {
-          // (r x u)_a = r_a1 u_a2 - r_a2 u_a1
-          tc += (double)rec[CMPC_REC_R + 4 * a1 + f] * (double)xs[v + a2] -
-                (double)rec[CMPC_REC_R + 4 * a2 + f] * (double)xs[v + a1];
-          sc += (double)xs[v + a];
-          v += 3;
+        for (int f = 0; f < 4; f++) {
+          ra1[f] = rec[CMPC_REC_R + 4 * a1 + f];
+          ra2[f] = rec[CMPC_REC_R + 4 * a2 + f];
+        }
+        const uint32_t st4 = *reinterpret_cast<const uint32_t*>(&sh.stance[4 * k]);
+        int v = sh.blkbase[k];
+#pragma unroll
+        for (int f = 0; f < 4; f++) {
+          const bool on = ((st4 >> (8 * f)) & 0xffu) != 0u;
+          // (r x u)_a = r_a1 u_a2 - r_a2 u_a1 (a swing foot's reads land on the next foot's
+          // variables, or past x's end inside the LDS block, and are discarded)
+          const double u0 = xs[v + a], u1 = xs[v + a1], u2 = xs[v + a2];
+          const double tf = (double)ra1[f] * u2 - (double)ra2[f] * u1;
+          tc += on ? tf : 0.0;
+          sc += on ? u0 : 0.0;
+          v += on ? 3 : 0;
+        }
+      } else {  // the per-foot branches (the branch-free form cost config 5 1.3 %, r04_l5)
+        int v = sh.blkbase[k];
+#pragma unroll
+        for (int f = 0; f < 4; f++) {
+          if (sh.stance[4 * k + f]) {
+            // (r x u)_a = r_a1 u_a2 - r_a2 u_a1
+            tc += (double)rec[CMPC_REC_R + 4 * a1 + f] * (double)xs[v + a2] -
+                  (double)rec[CMPC_REC_R + 4 * a2 + f] * (double)xs[v + a1];
+            sc += (double)xs[v + a];
+            v += 3;
+          }
         }
       }
       scr[S0 + 12 * k + a] = tc;
@@ -463,18 +488,33 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
       const double* R = scr;
       const double* Ii = scr + 9;
       const double xd = scr[18];
-      if (i < 3) {
+      if constexpr (NV <= 96) {
+        // branch-free over i (one instruction stream per wave; per-row branches cost 1 % at N = 16,
+        // r04_k16): i < 3 y_k,i = (I_w^-1 nu[6:9])_i; 3..5 nu[9 + i - 3] / m
+        const int ic = (i < 3) ? i : 0, il = (i < 3) ? 0 : i - 3;
+        double e1 = 0.0;
 #pragma unroll
         for (int m = 0; m < 3; m++) {
           const double nu = dt * mu[6 + m] + dth * (R[3 * m] * mu[0] + R[3 * m + 1] * mu[1] + R[3 * m + 2] * mu[2]);
-          ev += Ii[3 * i + m] * nu;
+          e1 += Ii[3 * ic + m] * nu;
         }
-      } else if (i == 3) {
-        ev = (dt * mu[9] + dth * (mu[3] + xd * mu[11]) + dt3 * xd * mu[5]) * (1.0 / 12.0);
-      } else if (i == 4) {
-        ev = (dt * mu[10] + dth * mu[4]) * (1.0 / 12.0);
+        const double x3 = (i == 3) ? xd : 0.0;
+        const double e2 = (dt * mu[9 + il] + dth * (mu[3 + il] + x3 * mu[11]) + dt3 * x3 * mu[5]) * (1.0 / 12.0);
+        ev = (i < 3) ? e1 : e2;
       } else {
-        ev = (dt * mu[11] + dth * mu[5]) * (1.0 / 12.0);
+        if (i < 3) {
+#pragma unroll
+          for (int m = 0; m < 3; m++) {
+            const double nu = dt * mu[6 + m] + dth * (R[3 * m] * mu[0] + R[3 * m + 1] * mu[1] + R[3 * m + 2] * mu[2]);
+            ev += Ii[3 * i + m] * nu;
+          }
+        } else if (i == 3) {
+          ev = (dt * mu[9] + dth * (mu[3] + xd * mu[11]) + dt3 * xd * mu[5]) * (1.0 / 12.0);
+        } else if (i == 4) {
+          ev = (dt * mu[10] + dth * mu[4]) * (1.0 / 12.0);
+        } else {
+          ev = (dt * mu[11] + dth * mu[5]) * (1.0 / 12.0);
+        }
       }
     }
     wbar();

@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "f_est", "f_est_smoothed", "f_est_static",
     "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
     "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
-    "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_read_timing", "cmpc_batch_estimate",
+    "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_enable_timing_every", "cmpc_batch_read_timing", "cmpc_batch_estimate",
     "cmpc_batch_assemble", "cmpc_batch_rollout", "cmpc_batch_admm",
     "cmpc_batch_quadprog",   # include/cmpc_quadprog.h
 )
@@ -98,6 +98,7 @@ def load_library(path: str = LIB_PATH):
     lib.cmpc_batch_stream.restype = ctypes.c_void_p
     lib.cmpc_last_error.restype = ctypes.c_char_p
     lib.cmpc_batch_enable_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.cmpc_batch_enable_timing_every.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     lib.cmpc_batch_read_timing.argtypes = [ctypes.c_void_p, _fp, _ip, _ip]
     lib.cmpc_batch_estimate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
@@ -349,10 +350,11 @@ class BatchSolver:
                                             _ptr(x), _ptr(f), _ptr(status), _ptr(iters), int(batch)),
                "cmpc_batch_quadprog")
 
-    def enable_timing(self, steps: int) -> None:
-        """Record HIP events around each size-class launch of the next ``steps`` solves."""
+    def enable_timing(self, steps: int, every: int = 1) -> None:
+        """Record HIP events around each size-class launch of the next ``steps`` solves (of every
+        ``every``-th solve only, ``steps`` of them, when ``every`` > 1)."""
         self._timing_steps = int(steps)
-        _check(self.lib.cmpc_batch_enable_timing(self._h, int(steps)), "enable_timing")
+        _check(self.lib.cmpc_batch_enable_timing_every(self._h, int(steps), int(every)), "enable_timing")
 
     def read_timing(self):
         """-> (ms [steps, 2] per class launch, class-1 overflow count of the last solve)."""
