@@ -165,6 +165,7 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.classified, hipEventDisableTiming);
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("fork event", e); }
   e = hipMalloc(&h->d_work, sizeof(int) * cmpc::work_ints(max_batch));
+  if (e == hipSuccess) e = hipMemset(h->d_work, 0, sizeof(int) * 2 * cmpc::kHdr);  // both list headers
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("hipMalloc(work)", e); }
   {
     float taps[cmpc::kGaussTaps];
@@ -295,7 +296,7 @@ extern "C" int cmpc_batch_read_timing(cmpc_batch* h, float* ms, int* steps_recor
   if (steps_recorded) *steps_recorded = h->ev_next;
   if (class1_overflow) {
     int c = 0;
-    e = hipMemcpy(&c, h->d_work, sizeof(int), hipMemcpyDeviceToHost);
+    e = hipMemcpy(&c, h->d_work + h->ctx.last_hdr * cmpc::kHdr, sizeof(int), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return fail("D2H", e);
     *class1_overflow = c;
   }

@@ -52,13 +52,15 @@ struct LocoParams {
 // since the general class went with CMPC_MAX_HORIZON = 20), 144, and 7: class-1 instances
 // with 60 < n <= 64 (the 64-wide class-1 build; n <= 60 runs in the 60-wide build over the
 // whole batch); 8: the 120-column wide build (97 <= n <= 120; the 128 build keeps 121..128).
-// d_work = [kHdr ints: cnt[0] total, cnt[1 + list] list lengths, cnt[kDeq + list] the persistent
-// wide workgroups' dequeue counters] [kLists lists of max_batch]
+// d_work = [2 headers of kHdr ints: cnt[0] total, cnt[1 + list] list lengths, cnt[kDeq + list] the
+// persistent wide workgroups' dequeue counters] [kLists lists of max_batch]. The solves alternate
+// over the two headers: each classify pass zeroes the header the next solve uses (the previous
+// solve, which used it, has joined by then), so no memset precedes a solve (zeroed at create)
 constexpr int kLists = 9;
 constexpr int kHdr = 32;
 constexpr int kDeq = 16;  // cnt[kDeq + list]: dequeue counter of a persistent class's workgroups
 static_assert(1 + kLists <= kDeq && kDeq + kLists <= kHdr, "list lengths and dequeue counters fit the header");
-inline size_t work_ints(int max_batch) { return kHdr + kLists * (size_t)max_batch; }
+inline size_t work_ints(int max_batch) { return 2 * kHdr + kLists * (size_t)max_batch; }
 // Side streams and events of one handle: the wider size classes run concurrently with class 1
 // (they are latency-bound: few instances, long serial solves). Two side streams: with the
 // handle's own stream that is three of the four hardware queues a process gets by default
@@ -69,12 +71,14 @@ struct LaunchCtx {
   hipEvent_t fork = nullptr;
   hipEvent_t classified = nullptr;  // the classify pass (on side 0) is done
   hipEvent_t join[kSideStreams] = {nullptr, nullptr};
+  int hdr = 0;       // header (0 / 1) of d_work the next solve's lists count into
+  int last_hdr = 0;  // header of the last solve (its cnt[0] for cmpc_batch_read_timing)
 };
 // ev (optional): 3 events recorded on `stream`: ev[0] before class 1, ev[1] after it, ev[2]
 // after the wider classes (side streams) have joined.
 hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float* d_forces,
                         uint8_t* d_status, int32_t* d_iters, int* d_work, int max_batch,
-                        hipStream_t stream, const LaunchCtx& ctx, hipEvent_t* ev = nullptr);
+                        hipStream_t stream, LaunchCtx& ctx, hipEvent_t* ev = nullptr);
 // per-class launchers (cmpc_class1.hip, cmpc_wide_w*.hip)
 hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* in_list, const int* in_count,

@@ -55,6 +55,9 @@
 #define CMPC_WIDE_REFINE 1
 #endif
 // refinements per instance at most, and the constraint tolerance (x x_max) after one
+#ifndef CMPC_WIDE_PRIO  // s_setprio of the wide classes' waves (0: the default priority)
+#define CMPC_WIDE_PRIO 0
+#endif
 #ifndef CMPC_DIAG_REF_SKIP  // diagnostic builds: skip refinement phases (bit 0..4 = A..E; wrong results)
 #define CMPC_DIAG_REF_SKIP 0
 #endif
@@ -1472,6 +1475,10 @@ template <int NV, bool PERSIST, bool REFINE>
 __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGPR_ATTR void cmpc_solve_w_kernel(
     WideArgs A) {
   __shared__ SharedW<NV> sh;
+#if CMPC_WIDE_PRIO > 0
+  // issue priority of this workgroup's waves over the class-1 waves sharing their SIMDs
+  __builtin_amdgcn_s_setprio(CMPC_WIDE_PRIO);
+#endif
   const int count = *A.in_count;
   if constexpr (!PERSIST) {  // one workgroup per possible list entry
     const int b = blockIdx.x;

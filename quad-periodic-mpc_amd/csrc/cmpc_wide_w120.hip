@@ -11,6 +11,9 @@
 #ifndef CMPC_WIDE_REFINE
 #define CMPC_WIDE_REFINE 0  // N <= 10 (no refinement); the refining builds: cmpc_wide_w120r.hip, w120pr.hip
 #endif
+#ifndef CMPC_WIDE_PRIO
+#define CMPC_WIDE_PRIO 1  // N <= 10: issue priority over the class-1 waves (config 2 +1.9 %, config 3 +0.2 %, r04_p)
+#endif
 #include "cmpc_wide.h"
 
 namespace cmpc {
