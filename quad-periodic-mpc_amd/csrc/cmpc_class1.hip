@@ -26,6 +26,9 @@
 
 #include "cmpc_common.h"
 
+#ifndef CMPC_W1_WAVES_60  // the 60-wide build's occupancy target (A/B builds; 5 measured config 3 -18 %, r04_q)
+#define CMPC_W1_WAVES_60 4
+#endif
 #ifndef CMPC_W1_WAVES_PER_EU
 #define CMPC_W1_WAVES_PER_EU 4
 #endif
@@ -851,7 +854,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 }  // namespace
 
 template <int NV>
-__global__ __launch_bounds__(64, CMPC_W1_WAVES_PER_EU) void cmpc_solve_c1_kernel(
+__global__ __launch_bounds__(64, NV == 60 ? CMPC_W1_WAVES_60 : CMPC_W1_WAVES_PER_EU) void cmpc_solve_c1_kernel(
     const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
     uint8_t* __restrict__ status, int32_t* __restrict__ iters, const int* __restrict__ in_list,
     const int* __restrict__ in_count, int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
