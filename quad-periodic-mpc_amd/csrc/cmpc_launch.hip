@@ -107,15 +107,18 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   const bool split60 = (n_max <= 64) || (batch >= 16384);
   const int c1_nv = (n_max <= 60 || split60) ? 60 : 64;
   if (n_max > 64) {
-    // From 16384 instances the classify pass runs on side 0 beside class 1 (which needs no list:
-    // it skips the instances above its row width itself), side 1 waiting for the lists; below,
-    // on the handle's stream ahead of everything. Batch sweep of both placements with the final
+    // From 16384 instances (and up to 4096) the classify pass runs on side 0 beside class 1 (which
+    // needs no list: it skips the instances above its row width itself), side 1 waiting for the
+    // lists; in between, on the handle's stream ahead of everything. Batch sweep of both placements with the final
     // kernels (profiles/r03_ab/sweep2): beside class 1 +2 % at 16384 .. 131072 instances, within
     // noise below. CMPC_CLASSIFY_SIDE=0/1 forces either placement (A/B).
     static const int cls_env = diag_knob("CMPC_CLASSIFY_SIDE", -1);
     // (Round 4 also measured the 80-column class launched ahead of class 1 as a persistent grid
     // resident before class 1 starts: config 3 -1 to -3 %, dropped.)
-    const bool cls_side = (cls_env < 0) ? (batch >= 16384) : (cls_env == 1);
+    // Round-4 sweep (profiles/r04_ab/r04_ks, beside vs ahead): 2048 +2.3 %, 4096 (config 2)
+    // +3.2 %, 6144 0, 8192 -2 %, 12288 -1.5 %: beside at the smallest batches too, where class 1
+    // starting without the classify pass's queue hop ahead of it pays most
+    const bool cls_side = (cls_env < 0) ? (batch >= 16384 || batch <= 4096) : (cls_env == 1);
     hipStream_t cs = cls_side ? ctx.side[0] : stream;
     if (cls_side) {
       if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
