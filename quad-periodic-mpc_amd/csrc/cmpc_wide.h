@@ -58,6 +58,9 @@
 #ifndef CMPC_WIDE_PRIO  // s_setprio of the wide classes' waves (0: the default priority)
 #define CMPC_WIDE_PRIO 0
 #endif
+#ifndef CMPC_DIAG_REF_LDSREC
+#define CMPC_DIAG_REF_LDSREC 0
+#endif
 #ifndef CMPC_DIAG_REF_SKIP  // diagnostic builds: skip refinement phases (bit 0..4 = A..E; wrong results)
 #define CMPC_DIAG_REF_SKIP 0
 #endif
@@ -286,8 +289,13 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
   // of the active-set loop and kept live across every trip. The fp64 scalars come from the kernel
   // arguments (SGPRs) or the LDS, never long-lived VGPRs: the 96-column class has 48 VGPRs beside
   // its J row
+#if CMPC_DIAG_REF_LDSREC  // diagnostic: the phases read LDS garbage in place of the record (timing only)
+  const float* rec = reinterpret_cast<const float*>(&sh.P[0]);
+  (void)rec_in;
+#else
   const float* rec = rec_in;
   asm volatile("" : "+s"(rec));
+#endif
   double* scr = reinterpret_cast<double*>(&sh.P[G::O_RINV]);
   const int N = P.N;
   const double dt = P.dt64, dth = P.dth64, dt3 = P.dt3_64;
