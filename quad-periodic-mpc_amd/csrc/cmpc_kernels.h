@@ -47,11 +47,11 @@ struct LocoParams {
 };
 
 // Scratch ints needed by launch_solve for max_batch instances.
-// d_work: [0] instances with n > 64, [1 + list] lengths of the class lists, then the lists of
-// max_batch entries each. Instance lists of the classify pass: 80, 96, 128, 192, 256, (5: unused
-// since the general class went with CMPC_MAX_HORIZON = 20), 144, and 7: class-1 instances
-// with 60 < n <= 64 (the 64-wide class-1 build; n <= 60 runs in the 60-wide build over the
-// whole batch); 8: the 120-column wide build (97 <= n <= 120; the 128 build keeps 121..128).
+// d_work: [0] instances above class 1's build, [1 + list] lengths of the class lists, then the
+// lists of max_batch entries each. Instance lists of the classify pass: 80, 96, 128, 192, 256,
+// 5: class 1's own instances from N = 11 (n <= its row width; up to N = 10 it runs over the whole
+// batch), 144, and 7: class-1 instances with 60 < n <= 64 (the 64-wide class-1 build beside the
+// 60-wide one); 8: the 120-column wide build (97 <= n <= 120; the 128 build keeps 121..128).
 // d_work = [2 headers of kHdr ints: cnt[0] total, cnt[1 + list] list lengths, cnt[kDeq + list] the
 // persistent wide workgroups' dequeue counters] [kLists lists of max_batch]. The solves alternate
 // over the two headers: each classify pass zeroes the header the next solve uses (the previous

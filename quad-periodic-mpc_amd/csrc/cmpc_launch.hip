@@ -22,7 +22,8 @@ namespace {
 __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restrict__ recs, int batch,
                                                            KParams P, int* __restrict__ cnt,
                                                            int* __restrict__ lists, int max_batch,
-                                                           int c1_max, int* __restrict__ next_hdr) {
+                                                           int c1_max, int* __restrict__ next_hdr,
+                                                           int c1_listed) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   if (blockIdx.x == 0 && threadIdx.x < kHdr) next_hdr[threadIdx.x] = 0;  // the next solve's counters
@@ -41,12 +42,15 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
       }
     }
     const int n = 3 * nfs;
-    cls = (n <= c1_max) ? -1 : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 120) ? 8
+    // c1_listed (N >= 11, where few instances have n <= 64): class 1 runs over list 5 instead of
+    // the whole batch, so the rest never stage their records only to exit
+    cls = (n <= c1_max) ? (c1_listed ? 5 : -1) : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 120) ? 8
         : (n <= 128) ? 2 : (n <= 144) ? 6 : (n <= 192) ? 3 : 4;
   }
   const unsigned long long any = __ballot(cls >= 0);
   if (any == 0ull) return;
-  if (lane == 0) atomicAdd(&cnt[0], __popcll(any));
+  const unsigned long long wide = __ballot(cls >= 0 && cls != 5);  // cnt[0]: n above class 1's build
+  if (lane == 0 && wide) atomicAdd(&cnt[0], __popcll(wide));
 #pragma unroll
   for (int c = 0; c < kLists; c++) {
     const unsigned long long m = __ballot(cls == c);
@@ -68,7 +72,9 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
 // (the same threshold as class 1's split) the drains are short and every class is one-per-entry
 // (config 2: 11.3 M -> 11.7 M QP/s).
 // CMPC_WIDE_FORM (A/B): 1 every class one-per-entry, 2 every class persistent.
-// (Only the class holding 6 N itself one-per-entry measured -0.3 % at config 3, round 4.)
+// (Round 4: only the class holding 6 N itself one-per-entry measured -0.3 % at config 3; the same
+// with the 80 class kept one-per-entry at N <= 10, i.e. the 128 class persistent at N = 20 and
+// the 120 class at N = 16, -1.0 % at config 5, +0.3 % at N = 16, profiles/r04_ab/r04_t*.)
 bool one_per_entry(int lo, int hi, int N, int batch) {
   static const int form = diag_knob("CMPC_WIDE_FORM", 0);
   if (form == 1 || batch < 16384) return true;
@@ -79,6 +85,9 @@ bool one_per_entry(int lo, int hi, int N, int batch) {
 
 }  // namespace
 
+#ifndef CMPC_C1_WHOLE_BATCH  // A/B builds: class 1 over the whole batch at every horizon (round 3)
+#define CMPC_C1_WHOLE_BATCH 0
+#endif
 #ifndef CMPC_HDR_MEMSET
 #define CMPC_HDR_MEMSET 0
 #endif
@@ -106,6 +115,11 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   // chain (config 2, batch 4096: 11.2 M -> 9.9 M), so one 64-wide launch takes all n <= 64.
   const bool split60 = (n_max <= 64) || (batch >= 16384);
   const int c1_nv = (n_max <= 60 || split60) ? 60 : 64;
+  // from N = 11 the trot size 6N is above class 1's rows and few instances reach class 1: it runs
+  // over a classify list (list 5) instead of the whole batch (config 5: 65536 record stagings and
+  // exits per step, 84 MB)
+  const bool c1_listed = 6 * P.N > 64 && !CMPC_C1_WHOLE_BATCH;
+  bool cls_side_used = false;
   if (n_max > 64) {
     // From 16384 instances (and up to 4096) the classify pass runs on side 0 beside class 1 (which
     // needs no list: it skips the instances above its row width itself), side 1 waiting for the
@@ -119,13 +133,14 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // +3.2 %, 6144 0, 8192 -2 %, 12288 -1.5 %: beside at the smallest batches too, where class 1
     // starting without the classify pass's queue hop ahead of it pays most
     const bool cls_side = (cls_env < 0) ? (batch >= 16384 || batch <= 4096) : (cls_env == 1);
+    cls_side_used = cls_side;
     hipStream_t cs = cls_side ? ctx.side[0] : stream;
     if (cls_side) {
       if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(ctx.side[0], ctx.fork, 0)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 63) / 64), dim3(64), 0, cs,
-                       d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr);
+                       d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr, c1_listed ? 1 : 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     ctx.last_hdr = ctx.hdr;
     if (!CMPC_HDR_MEMSET) ctx.hdr ^= 1;
@@ -198,8 +213,16 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
   // class 1 over the whole batch (it skips instances with n > its row width)
-  e = launch_class1(c1_nv, d_recs, batch, P, d_forces, d_status, d_iters, nullptr, nullptr, nullptr,
-                    nullptr, batch, stream);
+  if (c1_listed) {
+    // class 1 over the classify list of n <= its row width (one workgroup per possible entry,
+    // surplus ones exit after reading the count): behind the classify pass
+    if (cls_side_used && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
+    e = launch_class1(c1_nv, d_recs, batch, P, d_forces, d_status, d_iters, list[5], &cnt[6], nullptr,
+                      nullptr, batch, stream);
+  } else {
+    e = launch_class1(c1_nv, d_recs, batch, P, d_forces, d_status, d_iters, nullptr, nullptr, nullptr,
+                      nullptr, batch, stream);
+  }
   if (e != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (n_max > 64) {
