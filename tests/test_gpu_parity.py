@@ -288,6 +288,30 @@ def test_single_instance_fast_path_bitwise(cm, solver_mod, N, frac):
         s.close()
 
 
+@pytest.mark.parametrize("N", [10, 16])
+def test_handle_reuse_alternating_batches(cm, solver_mod, N):
+    """One handle solving batches of alternating size (each classify pass zeroes the list header
+    the next solve uses, cmpc_launch.hip; from N = 11 class 1 runs over a classify list): every
+    solve must equal the same records solved by a fresh handle, bit for bit, and the first batch
+    solved again at the end must reproduce itself."""
+    prm = cm.make_params(N)
+    sizes = [16384, 3000, 100, 16384, 7000]
+    recs = [cm.make_instances(b, N, seed=9100 + 17 * i + N, random_contact_frac=1.0)
+            for i, b in enumerate(sizes)]
+    s = solver_mod.BatchSolver(prm, max_batch=max(sizes))
+    try:
+        got = [s.solve_host(r) for r in recs]
+        again = s.solve_host(recs[0])
+    finally:
+        s.close()
+    for r, (f, st, it) in zip(recs, got):
+        f1, st1, it1 = gpu_solve(solver_mod, prm, r)
+        assert (st == 0).all(), np.bincount(st)
+        np.testing.assert_array_equal(f, f1)
+        np.testing.assert_array_equal(it, it1)
+    np.testing.assert_array_equal(again[0], got[0][0])
+
+
 @pytest.mark.parametrize("N", [10, 16, 20])
 def test_batch_size_invariance(cm, solver_mod, N):
     """The same record gets the same forces whatever batch it is solved in. The launch
