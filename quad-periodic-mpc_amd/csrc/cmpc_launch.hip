@@ -122,10 +122,10 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   bool cls_side_used = false;
   if (n_max > 64) {
     // From 16384 instances (and up to 4096) the classify pass runs on side 0 beside class 1 (which
-    // needs no list: it skips the instances above its row width itself), side 1 waiting for the
-    // lists; in between, on the handle's stream ahead of everything. Batch sweep of both placements with the final
-    // kernels (profiles/r03_ab/sweep2): beside class 1 +2 % at 16384 .. 131072 instances, within
-    // noise below. CMPC_CLASSIFY_SIDE=0/1 forces either placement (A/B).
+    // needs no list up to N = 10: it skips the instances above its row width itself), side 1
+    // waiting for the lists; in between, on the handle's stream ahead of everything. Round-3 batch
+    // sweep (profiles/r03_ab/sweep2): beside class 1 +2 % at 16384 .. 131072 instances.
+    // CMPC_CLASSIFY_SIDE=0/1 forces either placement (A/B).
     static const int cls_env = diag_knob("CMPC_CLASSIFY_SIDE", -1);
     // (Round 4 also measured the 80-column class launched ahead of class 1 as a persistent grid
     // resident before class 1 starts: config 3 -1 to -3 %, dropped.)
@@ -212,7 +212,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       return e;
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
-  // class 1 over the whole batch (it skips instances with n > its row width)
+  // class 1: up to N = 10 over the whole batch (it skips the instances above its row width
+  // itself), from N = 11 over list 5
   if (c1_listed) {
     // class 1 over the classify list of n <= its row width (one workgroup per possible entry,
     // surplus ones exit after reading the count): behind the classify pass
