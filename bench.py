@@ -391,8 +391,8 @@ def scaling_model(args, cm, dev, sync):
     out_b = 4 * 12 * N
     recs_all = torch.from_numpy(cm.make_instances(G_total, N, random_contact_frac=args.random_contact_frac)).to(dev)
     rows, t1 = [], None
-    def timed_pieces(local, chunks, lead=None):
-        pipe = par.RootPipeline(prm, local, chunks=chunks, device=dev, lead=lead)
+    def timed_pieces(local, chunks):
+        pipe = par.RootPipeline(prm, local, chunks=chunks, device=dev)
         recs = recs_all[:local]
         for _ in range(3):
             pipe.step(recs)
@@ -410,15 +410,13 @@ def scaling_model(args, cm, dev, sync):
     for G in (1, 2, 4, 8):
         local = G_total // G
         # the pieces a G-rank run cuts each rank's shard into (world 1 itself solves in one piece)
-        lead = par.auto_lead(local, G)
-        t_solve, pieces = timed_pieces(local, 2 if lead else par.auto_chunks(local, G), lead)
+        t_solve, pieces = timed_pieces(local, par.auto_chunks(local, G))
         row = {"gpus": G, "per_rank_instances": local, "pieces": len(pieces),
-               "piece_instances": pieces[0] if not lead else list(pieces),
-               "t_solve_ms_measured": round(t_solve * 1e3, 4)}
-        if G > 1:   # the other piece plan, for comparison (pieces alternate over two handles)
+               "piece_instances": pieces[0], "t_solve_ms_measured": round(t_solve * 1e3, 4)}
+        if G > 1:   # the other piece count, for comparison (pieces alternate over two handles)
             alt = 1 if len(pieces) > 1 else 2
             t_alt, _ = timed_pieces(local, alt)
-            row["t_solve_ms_measured_with_%d_pieces" % alt + ("_equal" if alt == 2 else "")] = round(t_alt * 1e3, 4)
+            row["t_solve_ms_measured_with_%d_pieces" % alt] = round(t_alt * 1e3, 4)
         if G == 1:
             t1 = t_solve
             row.update(t_model_ms=round(t_solve * 1e3, 4), speedup=1.0)
@@ -490,8 +488,6 @@ def main():
     ap.add_argument("--chunks", type=int, default=None,
                     help="config-4 pipeline pieces per rank (default: parallel.auto_chunks)")
     ap.add_argument("--horizon", type=int, default=None)
-    ap.add_argument("--lead-piece", type=int, default=None,
-                    help="config 4: first piece of each rank's shard (with --chunks 2)")
     ap.add_argument("--random-contact-frac", type=float, default=0.25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip end-to-end / solve-only legs")
@@ -544,7 +540,7 @@ def main():
     if config == 4:
         par = importlib.import_module("quad-periodic-mpc_amd.parallel")
         G = args.global_batch or 262144
-        pipe = par.RootPipeline(prm, G, chunks=args.chunks, device=dev, lead=args.lead_piece,
+        pipe = par.RootPipeline(prm, G, chunks=args.chunks, device=dev,
                                 solve_fn=plumbing_solve(N) if args.dry_run else None)
         recs_root = None
         if rank == 0:

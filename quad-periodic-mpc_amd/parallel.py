@@ -172,35 +172,13 @@ def auto_chunks(local_batch: int, world: int = 2, min_piece: int = MIN_PIECE,
     return max(1, min(max_chunks, local_batch // max(1, min_piece)))
 
 
-# A short first piece for shards that auto_chunks keeps whole (4 and 8 ranks): its records cross
-# xGMI in a few microseconds, its solve starts at once and the rest of the shard follows on the
-# second solver lane while its own records are still in flight. Measured on one MI355X
-# (scripts/piece_probe.py, profiles/r04_ab/r04_pp): 32768 instances in one solve 0.911 ms,
-# 4096 + 28672 on two lanes 0.888 ms (on one lane, back to back, 1.036 ms).
-LEAD_PIECE = 4096
-
-
-def auto_lead(local_batch: int, world: int = 2, lead: int = LEAD_PIECE) -> Optional[int]:
-    """Size of the short first piece of a rank's shard (the shard then goes in two pieces), or
-    None: only where there is traffic to hide (world > 1), auto_chunks keeps the shard whole and
-    the shard holds at least four lead pieces (262144 over 4 / 8 ranks -> 4096)."""
-    if world <= 1 or auto_chunks(local_batch, world) != 1 or local_batch < 4 * lead:
-        return None
-    return lead
-
-
-def _chunk_plan(batch: int, world: int, chunks: int, lead: Optional[int] = None):
+def _chunk_plan(batch: int, world: int, chunks: int):
     """Per rank r and chunk c: rows [a_rc, b_rc) of the global batch (contiguous rank shards,
-    each split into ``chunks`` contiguous pieces: equal ones, or with ``lead`` and two chunks a
-    first piece of ``lead`` rows and the rest) and S_c = the largest piece c over ranks (the
+    each split into ``chunks`` contiguous pieces) and S_c = the largest piece c over ranks (the
     collective size; shorter pieces are padded)."""
     plan = []
     for r in range(world):
         a, b = shard_bounds(batch, world, r)
-        if lead and chunks == 2:
-            k = min(int(lead), b - a)
-            plan.append([(a, a + k), (a + k, b)])
-            continue
         plan.append([(a + lo, a + hi) for lo, hi in
                      (shard_bounds(b - a, chunks, c) for c in range(chunks))])
     sizes = [max(plan[r][c][1] - plan[r][c][0] for r in range(world)) for c in range(chunks)]
@@ -232,7 +210,7 @@ class RootPipeline:
 
     def __init__(self, params, global_batch: int, chunks: Optional[int] = None, *, group=None,
                  device=None, src: int = 0, solve_fn=None, record_words: Optional[int] = None,
-                 lanes: Optional[int] = None, lead: Optional[int] = None):
+                 lanes: Optional[int] = None):
         from .records import record_words as _rw
         self.params = params
         self.N = params.horizon
@@ -241,17 +219,10 @@ class RootPipeline:
         self.group = group
         self.src = src
         self.world, self.rank = _group_info(group)
-        if chunks is None:   # adaptive: pieces of >= MIN_PIECE instances (auto_chunks), or a
-            # short lead piece and the rest where the shard stays whole (auto_lead)
-            local_max = max(shard_sizes(self.batch, self.world))
-            chunks = auto_chunks(local_max, self.world)
-            if lead is None:
-                lead = auto_lead(local_max, self.world)
-                if lead:
-                    chunks = 2
+        if chunks is None:   # adaptive: pieces of >= MIN_PIECE instances (auto_chunks)
+            chunks = auto_chunks(max(shard_sizes(self.batch, self.world)), self.world)
         self.chunks = max(1, min(int(chunks), max(1, self.batch // max(1, self.world))))
-        self.lead = int(lead) if (lead and self.chunks == 2) else None
-        self.plan, self.sizes = _chunk_plan(self.batch, self.world, self.chunks, self.lead)
+        self.plan, self.sizes = _chunk_plan(self.batch, self.world, self.chunks)
         self.start, self.stop = shard_bounds(self.batch, self.world, self.rank)
         self.local_batch = self.stop - self.start
         self.device = device

@@ -36,16 +36,6 @@ def test_config4_sharded_equals_single(gpus, gb, chunks):
     assert many["status_counts"] == {"ok": gb}
 
 
-def test_config4_lead_piece_sharded_equals_single():
-    """The short-first-piece plan (parallel.auto_lead, used at 4 and 8 ranks) at world 2 over gloo:
-    the gathered forces equal a world-1 run with the same plan bit for bit."""
-    args = ("--global-batch", "20000", "--chunks", "2", "--lead-piece", "1000")
-    one = _bench("--config", "4", *args)
-    many = _bench("--gpus", "2", *args)
-    assert many["n_gpus"] == 2 and many["forces_digest"] == one["forces_digest"]
-    assert many["status_counts"] == {"ok": 20000}
-
-
 def test_weak_mode_shards_reproduce_ids(cm):
     """Per-rank generation of instance ids [r*B, (r+1)*B) equals slices of one generation."""
     import numpy as np

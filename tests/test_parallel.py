@@ -85,21 +85,3 @@ def test_shard_bounds_cover_batch():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         par.shard_bounds(10, 2, 2)
-
-
-def test_lead_piece_plan():
-    """auto_lead: a short first piece only where a shard would otherwise go whole at world > 1;
-    _chunk_plan with a lead covers every shard exactly, first piece = lead rows."""
-    par = importlib.import_module("quad-periodic-mpc_amd.parallel")
-    assert par.auto_lead(262144, 1) is None                  # world 1: nothing to hide
-    assert par.auto_lead(131072, 2) is None                  # two equal pieces already
-    assert par.auto_lead(65536, 4) == par.LEAD_PIECE
-    assert par.auto_lead(32768, 8) == par.LEAD_PIECE
-    assert par.auto_lead(3 * par.LEAD_PIECE, 8) is None      # too small to split
-    for batch, world, lead in ((262144, 8, 4096), (10007, 3, 1000), (5, 2, 4)):
-        plan, sizes = par._chunk_plan(batch, world, 2, lead)
-        for r in range(world):
-            a, b = par.shard_bounds(batch, world, r)
-            (a0, b0), (a1, b1) = plan[r]
-            assert (a0, b1) == (a, b) and b0 == a1 and b0 - a0 == min(lead, b - a)
-        assert sizes == [max(p[c][1] - p[c][0] for p in plan) for c in range(2)]
