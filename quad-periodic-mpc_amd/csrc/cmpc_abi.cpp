@@ -456,7 +456,7 @@ namespace {
 struct SingleState {
   std::mutex mu;
   cmpc_params cfg{};              // problem_configuration (convexMPC_interface.cpp:10)
-  bool configured = false;
+  bool configured = false;        // the last setup_problem asked for a horizon in 1..CMPC_MAX_HORIZON
   // update_data_t fields (convexMPC_interface.h:23-41)
   float p[3]{}, v[3]{}, q[4]{}, w[3]{}, r[12]{};
   float roll = 0, pitch = 0, yaw = 0, alpha = 0, x_drag = 0;
@@ -606,8 +606,10 @@ void solve_single(SingleState& s) {
   for (int i = 0; i < 6; i++) f_est_smoothed[i] = 0.95f * f_est_smoothed[i] + 0.05f * f_est[i];
   f_est_static[3] = 0.97f * f_est_static[3] + 0.03f * f_ext[3];
   const bool admm = (s.use_jcqp == 1 || s.use_jcqp == 2);
-  // qpOASES failure: print and keep the previous solution (SolverMPC.cpp:967); the reference
-  // keeps JCQP's solution whatever its residual (status 0 or 1)
+  // a failed qpOASES-equivalent solve prints as the reference does (SolverMPC.cpp:965-968) and
+  // stores what the kernel wrote for it (zeros for every force); a failed ADMM
+  // solve keeps the previous solution. The reference keeps JCQP's solution whatever its residual
+  // (status 0 or 1).
   if (admm ? (st != 0 && st != 1) : (st != CMPC_OK)) {
     std::printf("failed to solve!\n");
     if (admm) return;
@@ -624,12 +626,31 @@ extern "C" void setup_problem(double dt, int horizon, double mu, double f_max) {
   g.cfg.horizon = horizon;
   g.cfg.mu = (float)mu;
   g.cfg.f_max = (float)f_max;
-  g.configured = true;
-  // resize_qp_mats (SolverMPC.cpp:149-250): the reference re-allocates q_soln here
-  g.traj.assign(12 * (horizon > 0 ? horizon : 1) + 12 * CMPC_MAX_HORIZON, 0.f);
-  g.gait.assign(4 * CMPC_MAX_HORIZON + 4, 0);
-  if (horizon > 19) std::fprintf(stderr, "[cmpc] horizon %d > 19: reference c2qp would throw; cap lifted\n", horizon);
+  // resize_qp_mats (SolverMPC.cpp:149-250). The staging holds the largest horizon the solver
+  // admits, whatever is asked here, so no later copy depends on this call's horizon.
+  g.traj.assign(12 * CMPC_MAX_HORIZON, 0.f);
+  g.gait.assign(4 * CMPC_MAX_HORIZON, 0);
+  g.configured = horizon >= 1 && horizon <= CMPC_MAX_HORIZON;
+  if (!g.configured)
+    // the reference throws from c2qp above 19 (SolverMPC.cpp:113-116) on the next solve; here
+    // every update_problem_data* call refuses until a valid setup_problem and get_solution keeps
+    // returning the previous solution
+    std::fprintf(stderr, "[cmpc] setup_problem: horizon %d outside 1..%d; solves are refused and "
+                 "the previous solution is kept\n", horizon, CMPC_MAX_HORIZON);
+  else if (horizon > 19)
+    std::fprintf(stderr, "[cmpc] horizon %d > 19: reference c2qp would throw; cap lifted\n", horizon);
 }
+
+namespace {
+// update_problem_data* before a valid setup_problem: nothing is copied (the staging holds
+// CMPC_MAX_HORIZON steps) and nothing is solved
+bool refuse_update(const char* who) {
+  if (g.configured) return false;
+  std::fprintf(stderr, "[cmpc] %s: horizon %d not configured (setup_problem with 1..%d first); "
+               "previous solution kept\n", who, g.cfg.horizon, CMPC_MAX_HORIZON);
+  return true;
+}
+}  // namespace
 
 extern "C" void update_solver_settings(int max_iter, double rho, double sigma, double solver_alpha,
                                        double terminate, double use_jcqp) {
@@ -647,6 +668,7 @@ extern "C" void update_problem_data_floats(float* p, float* v, float* q, float* 
                                            float pitch, float yaw, float* weights, float* state_trajectory,
                                            float alpha, int* gait) {
   std::lock_guard<std::mutex> lk(g.mu);
+  if (refuse_update("update_problem_data_floats")) return;
   const int N = g.cfg.horizon;
   g.alpha = alpha;
   g.roll = roll;
@@ -666,6 +688,7 @@ extern "C" void update_problem_data_floats(float* p, float* v, float* q, float* 
 extern "C" void update_problem_data(double* p, double* v, double* q, double* w, double* r, double yaw,
                                     double* weights, double* state_trajectory, double alpha, int* gait) {
   std::lock_guard<std::mutex> lk(g.mu);
+  if (refuse_update("update_problem_data")) return;
   const int N = g.cfg.horizon;
   for (int i = 0; i < 3; i++) { g.p[i] = (float)p[i]; g.v[i] = (float)v[i]; g.w[i] = (float)w[i]; }
   for (int i = 0; i < 4; i++) g.q[i] = (float)q[i];
@@ -685,5 +708,8 @@ void update_x_drag(float x_drag) {
 extern "C" double get_solution(int index) {
   std::lock_guard<std::mutex> lk(g.mu);
   if (!g.has_solved) return 0.f;
+  // the reference reads q_soln[index] unchecked (convexMPC_interface.cpp:156-162); past the last
+  // solve's 12N values this returns 0
+  if (index < 0 || (size_t)index >= g.q_soln.size()) return 0.0;
   return g.q_soln[index];
 }

@@ -269,6 +269,83 @@ def test_reference_call_protocol(cm, orc, solver_mod):
         assert rel_force_err(sol[None], g["q_ref"][i][None]).max() <= 1e-4
 
 
+def _abi_floats(solver_mod, cm, rec, N, prm, gait=None, traj=None):
+    gait = cm.unpack_gait(rec[None], N)[0].astype(np.int32) if gait is None else gait
+    traj = rec[32:32 + 12 * N] if traj is None else traj
+    solver_mod.update_problem_data_floats(rec[0:3], rec[3:6], rec[6:10], rec[10:13], rec[13:25],
+                                          rec[25], rec[26], rec[27], np.array(prm.weights),
+                                          traj, prm.alpha, gait)
+
+
+def _abi_doubles(solver_mod, cm, rec, N, prm, gait=None, traj=None):
+    gait = cm.unpack_gait(rec[None], N)[0].astype(np.int32) if gait is None else gait
+    traj = rec[32:32 + 12 * N] if traj is None else traj
+    solver_mod.update_problem_data(*(np.asarray(rec[a:b], np.float64) for a, b in
+                                     ((0, 3), (3, 6), (6, 10), (10, 13), (13, 25))),
+                                   float(rec[27]), np.array(prm.weights, np.float64),
+                                   np.asarray(traj, np.float64), float(prm.alpha), gait)
+
+
+@pytest.mark.parametrize("name", ["n10_mixed", "n16_trot"])
+def test_reference_call_protocol_double_variant(cm, orc, solver_mod, name):
+    """update_problem_data (the double-precision entry point, convexMPC_interface.cpp:89-107:
+    every array cast to float, roll / pitch not passed) through the reference ABI: the forces
+    match the golden qpOASES solution and equal the float entry point's bit for bit."""
+    g = load_golden(name)
+    prm = golden_params(cm, g)
+    N = prm.horizon
+    for i in range(3):
+        rec = g["records"][i]
+        solver_mod.setup_problem(prm.dt, N, prm.mu, prm.f_max)
+        solver_mod.update_x_drag(float(rec[28]))
+        solver_mod.update_solver_settings(100, 1e-7, 1e-8, 1.5, 1e-5, 0)
+        _abi_doubles(solver_mod, cm, rec, N, prm)
+        sol_d = np.array([solver_mod.get_solution(j) for j in range(12 * N)])
+        _abi_floats(solver_mod, cm, rec, N, prm)
+        sol_f = np.array([solver_mod.get_solution(j) for j in range(12 * N)])
+        np.testing.assert_array_equal(sol_d, sol_f)
+        if g["status"][i] == 0:
+            assert rel_force_err(sol_d[None], g["q_ref"][i][None]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("bad_N", [0, 21, 22, 24, 40])
+def test_reference_abi_rejects_horizon_beyond_max(cm, solver_mod, bad_N, capfd):
+    """setup_problem with a horizon outside 1..CMPC_MAX_HORIZON (the reference throws from c2qp
+    above 19, SolverMPC.cpp:113-116): both update_problem_data entry points are refused without
+    copying the caller's 12N trajectory / 4N gait arrays, and get_solution keeps returning the
+    previous solve's forces (0 past its 12N values); a valid setup_problem afterwards solves
+    again. Arrays sized for bad_N are passed, as a caller that trusts its horizon would."""
+    g = load_golden("n10_mixed")
+    prm = golden_params(cm, g)
+    rec = g["records"][5]
+    solver_mod.setup_problem(prm.dt, 10, prm.mu, prm.f_max)
+    solver_mod.update_x_drag(float(rec[28]))
+    solver_mod.update_solver_settings(100, 1e-7, 1e-8, 1.5, 1e-5, 0)
+    _abi_floats(solver_mod, cm, rec, 10, prm)
+    prev = np.array([solver_mod.get_solution(j) for j in range(120)])
+    assert rel_force_err(prev[None], g["q_ref"][5][None]).max() <= 1e-4
+    capfd.readouterr()
+    M = max(bad_N, 1)
+    big_traj = np.tile(rec[32:44], M).astype(np.float32)
+    big_gait = np.ones(4 * M, np.int32)
+    solver_mod.setup_problem(prm.dt, bad_N, prm.mu, prm.f_max)
+    _abi_floats(solver_mod, cm, rec, M, prm, gait=big_gait, traj=big_traj)
+    _abi_doubles(solver_mod, cm, rec, M, prm, gait=big_gait, traj=big_traj)
+    err = capfd.readouterr().err
+    assert "setup_problem: horizon" in err and err.count("previous solution kept") == 2, err
+    after = np.array([solver_mod.get_solution(j) for j in range(12 * M + 12)])
+    np.testing.assert_array_equal(after[:120], prev)
+    assert (after[120:] == 0).all()
+    assert solver_mod.get_solution(-1) == 0.0
+    # a valid configuration solves again (instance 6)
+    rec6 = g["records"][6]
+    solver_mod.setup_problem(prm.dt, 10, prm.mu, prm.f_max)
+    solver_mod.update_x_drag(float(rec6[28]))
+    _abi_floats(solver_mod, cm, rec6, 10, prm)
+    sol6 = np.array([solver_mod.get_solution(j) for j in range(120)])
+    assert rel_force_err(sol6[None], g["q_ref"][6][None]).max() <= 1e-4
+
+
 @pytest.mark.parametrize("N,frac", [(10, 0.5), (20, 1.0)])
 def test_single_instance_fast_path_bitwise(cm, solver_mod, N, frac):
     """batch == 1 from host memory takes the one-kernel fast path (host-counted size class, no
