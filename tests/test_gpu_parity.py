@@ -333,7 +333,7 @@ def test_reference_abi_rejects_horizon_beyond_max(cm, solver_mod, bad_N, capfd):
     _abi_doubles(solver_mod, cm, rec, M, prm, gait=big_gait, traj=big_traj)
     err = capfd.readouterr().err
     assert "setup_problem: horizon" in err and err.count("previous solution kept") == 2, err
-    after = np.array([solver_mod.get_solution(j) for j in range(12 * M + 12)])
+    after = np.array([solver_mod.get_solution(j) for j in range(max(12 * M, 120) + 12)])
     np.testing.assert_array_equal(after[:120], prev)
     assert (after[120:] == 0).all()
     assert solver_mod.get_solution(-1) == 0.0
