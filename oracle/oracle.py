@@ -165,12 +165,10 @@ def ct_mats64(rec: np.ndarray):
     return A, B, Q
 
 
-def fp64_solve(rec: np.ndarray, prm):
-    """The reference pipeline in float64 throughout: scipy expm discretisation, dense condensation
-    (SolverMPC.cpp:806-814), the same swing elimination, qpOASES on the float64 reduced QP.
-    Returns (q_soln [12N], qpOASES return value). This is the optimum the reference's fp32
-    pipeline approximates; at N = 20 the reference itself lands up to ~1e-4 (relative) from it
-    (scripts/exact_gap.py)."""
+def fp64_condense(rec: np.ndarray, prm):
+    """Float64 restatement of the condensation (SolverMPC.cpp:806-814) with scipy's expm
+    discretisation of c2qp (:96-107): the full qH [12N, 12N] and qg [12N] the reference's fp32
+    GEMMs approximate."""
     from scipy.linalg import expm
     N = prm.horizon
     c = condense(rec, prm, full=False)
@@ -198,6 +196,18 @@ def fp64_solve(rec: np.ndarray, prm):
         f[3] = rec[29]
     qH = 2 * (Bqp.T @ (w[:, None] * Bqp) + prm.alpha * np.eye(nu))
     qg = 2 * Bqp.T @ (w * (Aqp @ x0 + Qqp @ f - Xd))
+    return qH, qg
+
+
+def fp64_solve(rec: np.ndarray, prm):
+    """The reference pipeline in float64 throughout: scipy expm discretisation, dense condensation
+    (SolverMPC.cpp:806-814, fp64_condense), the same swing elimination, qpOASES on the float64
+    reduced QP. Returns (q_soln [12N], qpOASES return value). This is the optimum the reference's
+    fp32 pipeline approximates; at N = 20 the reference itself lands up to ~1e-4 (relative) from
+    it (scripts/exact_gap.py)."""
+    N = prm.horizon
+    nu = 12 * N
+    qH, qg = fp64_condense(rec, prm)
     red = reduce(rec, prm, qH.astype(np.float32), qg.astype(np.float32))
     keep = ~red["var_elim"]
     x, _, ri, _ = qpoases(qH[np.ix_(keep, keep)], qg[keep], red["A"], red["lb"], red["ub"],

@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcmpc_hip.so")
 OBJ = os.path.join(ROOT, "build", "obj")
 # one translation unit per kernel family so the large unrolled kernels compile in parallel
-SOURCES = ["cmpc_wide_w256.hip", "cmpc_wide_w192.hip", "cmpc_class1.hip", "cmpc_wide_w80.hip", "cmpc_wide_w96.hip",
+SOURCES = ["cmpc_tail.hip", "cmpc_wide_w256.hip", "cmpc_wide_w192.hip", "cmpc_class1.hip", "cmpc_wide_w80.hip", "cmpc_wide_w96.hip",
            "cmpc_wide_w120.hip", "cmpc_wide_w128.hip", "cmpc_wide_w144.hip", "cmpc_wide_w80p.hip",
            "cmpc_wide_w96p.hip", "cmpc_wide_w120p.hip", "cmpc_wide_w128p.hip", "cmpc_wide_w80r.hip",
            "cmpc_wide_w96r.hip", "cmpc_wide_w120r.hip", "cmpc_wide_w80pr.hip", "cmpc_wide_w96pr.hip",

@@ -386,6 +386,28 @@ static int host_reduced_size(const float* rec, int N, float f_max) {
   return 3 * nfs;
 }
 
+// The tail classes hand an instance whose active set outgrows 64 positions to the 80-column wide
+// class (cmpc_tail.hip); on the single-instance path that shows as the status byte kHandoffStatus:
+// re-launch the record (already on the device) in the wide class and read the result again
+static int single_handoff(cmpc_batch* h, int n, float* pin_out, int N, int32_t* iters = nullptr) {
+  uint8_t st = 0;
+  std::memcpy(&st, pin_out + 12 * N, 1);
+  if (st != cmpc::kHandoffStatus) return 0;
+  float* d_out = h->d_single_out;
+  uint8_t* d_st = reinterpret_cast<uint8_t*>(d_out + 12 * N);
+  hipError_t e;
+  if ((e = cmpc::launch_single(h->d_rec, n, h->kp, d_out, d_st, h->d_iters, h->d_one, h->stream, false)) !=
+      hipSuccess)
+    return fail("launch_single", e);
+  if ((e = hipMemcpyAsync(pin_out, d_out, (12 * N + 1) * sizeof(float), hipMemcpyDeviceToHost, h->stream)) !=
+      hipSuccess)
+    return fail("D2H", e);
+  if (iters && (e = hipMemcpyAsync(iters, h->d_iters, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+    return fail("D2H", e);
+  if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail("sync", e);
+  return 0;
+}
+
 // batch == 1 from host memory: one kernel of the instance's class, pinned copies, one D2H
 static int solve_single_host(cmpc_batch* h, const float* record, float* forces, uint8_t* status,
                              int32_t* iters) {
@@ -408,6 +430,7 @@ static int solve_single_host(cmpc_batch* h, const float* record, float* forces, 
   if (iters && (e = hipMemcpyAsync(iters, h->d_iters, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
     return fail("D2H", e);
   if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail("sync", e);
+  if (int r = single_handoff(h, n, pin_out, N, iters)) return r;
   std::memcpy(forces, pin_out, 12 * N * sizeof(float));
   if (status) std::memcpy(status, pin_out + 12 * N, 1);
   return 0;
@@ -552,6 +575,7 @@ int solve_single_device(SingleState& s, const float* rec, int N, float* forces, 
       hipSuccess)
     return fail("D2H", e);
   if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail("sync", e);
+  if (int r = single_handoff(h, n, pin_out, N)) return r;  // (f_est(3) at pin_out[12 N + 1] stays)
   std::memcpy(forces, pin_out, 12 * N * sizeof(float));
   std::memcpy(st, pin_out + 12 * N, 1);
   std::memcpy(&f_est[3], pin_out + 12 * N + 1, sizeof(float));

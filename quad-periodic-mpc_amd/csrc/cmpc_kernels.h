@@ -52,25 +52,30 @@ struct LocoParams {
 // 5: class 1's own instances from N = 11 (n <= its row width; up to N = 10 it runs over the whole
 // batch), 144, and 7: class-1 instances with 60 < n <= 64 (the 64-wide class-1 build beside the
 // 60-wide one); 8: the 120-column wide build (97 <= n <= 120; the 128 build keeps 121..128).
+// 9: the tail class (cmpc_tail.hip, N <= 10: 64 < n <= 72, one wavefront each); 10: the instances
+// it hands to the 80-column wide class (an active set past 64 positions).
 // d_work = [2 headers of kHdr ints: cnt[0] total, cnt[1 + list] list lengths, cnt[kDeq + list] the
 // persistent wide workgroups' dequeue counters] [kLists lists of max_batch]. The solves alternate
 // over the two headers: each classify pass zeroes the header the next solve uses (the previous
 // solve, which used it, has joined by then), so no memset precedes a solve (zeroed at create)
-constexpr int kLists = 9;
+constexpr int kLists = 11;
 constexpr int kHdr = 32;
 constexpr int kDeq = 16;  // cnt[kDeq + list]: dequeue counter of a persistent class's workgroups
 static_assert(1 + kLists <= kDeq && kDeq + kLists <= kHdr, "list lengths and dequeue counters fit the header");
 inline size_t work_ints(int max_batch) { return 2 * kHdr + kLists * (size_t)max_batch; }
 // Side streams and events of one handle: the wider size classes run concurrently with class 1
-// (they are latency-bound: few instances, long serial solves). Two side streams: with the
-// handle's own stream that is three of the four hardware queues a process gets by default
-// (GPU_MAX_HW_QUEUES), so no side stream shares a queue with class 1.
-constexpr int kSideStreams = 2;
+// (they are latency-bound: few instances, long serial solves). Three side streams (the third
+// carries only the tail class at N <= 10 below 131072 instances): with the handle's own stream
+// that is the four hardware queues a process gets by default (GPU_MAX_HW_QUEUES = 4), so no side
+// stream shares a queue with class 1. A process with two handles (parallel.RootPipeline's two
+// solver lanes) has eight streams over those four queues: the lanes' streams alias in pairs; the
+// lanes alternate pieces, so at most one lane's class 1 runs at a time.
+constexpr int kSideStreams = 3;
 struct LaunchCtx {
-  hipStream_t side[kSideStreams] = {nullptr, nullptr};
+  hipStream_t side[kSideStreams] = {nullptr, nullptr, nullptr};
   hipEvent_t fork = nullptr;
   hipEvent_t classified = nullptr;  // the classify pass (on side 0) is done
-  hipEvent_t join[kSideStreams] = {nullptr, nullptr};
+  hipEvent_t join[kSideStreams] = {nullptr, nullptr, nullptr};
   int hdr = 0;       // header (0 / 1) of d_work the next solve's lists count into
   int last_hdr = 0;  // header of the last solve (its cnt[0] for cmpc_batch_read_timing)
 };
@@ -100,8 +105,21 @@ CMPC_DECL_WIDE(144)
 CMPC_DECL_WIDE(192)
 CMPC_DECL_WIDE(256)
 #undef CMPC_DECL_WIDE
+// the tail class (cmpc_tail.hip): 8 tail rows beside class 1's 64 (n <= 72), one wavefront per
+// instance over its list, one workgroup per possible entry; an instance whose active set outgrows
+// 64 positions is appended to ovf_list (batched) or, with ovf_list == nullptr, gets status
+// kHandoffStatus (single-instance path: the host re-launches it in the wide class,
+// launch_single(..., allow_tail = false))
+constexpr uint8_t kHandoffStatus = 0xFE;
+hipError_t launch_tail(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
+                       int32_t* d_iters, const int* in_list, const int* in_count, int* ovf_list,
+                       int* ovf_count, int grid, hipStream_t stream);
+// the reduced sizes the tail class takes from the 80-column wide class: 64 < n <= 72 at N <= 10
+// (the horizons without the fp64 refinement of the wide classes)
+inline bool tail_class(const KParams& P, int n) { return !P.refine && n > 64 && n <= 72; }
 hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_forces,
-                         uint8_t* d_status, int32_t* d_iters, const int* d_one, hipStream_t stream);
+                         uint8_t* d_status, int32_t* d_iters, const int* d_one, hipStream_t stream,
+                         bool allow_tail = true);
 // config 5 estimator (cmpc_estimator.hip). d_gauss: the two normalised float Gaussian kernels
 // of gaussian_filter (sigma 7: 43 taps, then sigma 27: 163 taps), built on the host exactly as
 // SolverMPC.cpp:404-418 builds them.

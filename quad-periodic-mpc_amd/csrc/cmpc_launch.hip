@@ -23,7 +23,7 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
                                                            KParams P, int* __restrict__ cnt,
                                                            int* __restrict__ lists, int max_batch,
                                                            int c1_max, int* __restrict__ next_hdr,
-                                                           int c1_listed) {
+                                                           int c1_listed, int tail) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   if (blockIdx.x == 0 && threadIdx.x < kHdr) next_hdr[threadIdx.x] = 0;  // the next solve's counters
@@ -44,7 +44,10 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
     const int n = 3 * nfs;
     // c1_listed (N >= 11, where few instances have n <= 64): class 1 runs over list 5 instead of
     // the whole batch, so the rest never stage their records only to exit
-    cls = (n <= c1_max) ? (c1_listed ? 5 : -1) : (n <= 64) ? 7 : (n <= 80) ? 0 : (n <= 96) ? 1 : (n <= 120) ? 8
+    // tail (N <= 10): 64 < n <= 72 in the one-wave tail class (list 9) instead of the 80-column
+    // wide class (list 0)
+    cls = (n <= c1_max) ? (c1_listed ? 5 : -1) : (n <= 64) ? 7 : (n <= 80) ? ((tail && n <= 72) ? 9 : 0)
+        : (n <= 96) ? 1 : (n <= 120) ? 8
         : (n <= 128) ? 2 : (n <= 144) ? 6 : (n <= 192) ? 3 : 4;
   }
   const unsigned long long any = __ballot(cls >= 0);
@@ -75,6 +78,10 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
 // (Round 4: only the class holding 6 N itself one-per-entry measured -0.3 % at config 3; the same
 // with the 80 class kept one-per-entry at N <= 10, i.e. the 128 class persistent at N = 20 and
 // the 120 class at N = 16, -1.0 % at config 5, +0.3 % at N = 16, profiles/r04_ab/r04_t*.)
+// workgroups of the 80-column class's persistent launch over the tail classes' hand-offs (an
+// active set past 64 positions: none in any measured workload)
+constexpr int kHandoffGrid = 16;
+
 bool one_per_entry(int lo, int hi, int N, int batch) {
   static const int form = diag_knob("CMPC_WIDE_FORM", 0);
   if (form == 1 || batch < 16384) return true;
@@ -119,6 +126,25 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   // over a classify list (list 5) instead of the whole batch (config 5: 65536 record stagings and
   // exits per step, 84 MB)
   const bool c1_listed = 6 * P.N > 64 && !CMPC_C1_WHOLE_BATCH;
+  // 64 < n <= 80 in the one-wave tail classes (N <= 10, no refinement; cmpc_tail.hip).
+  // CMPC_TAIL=0 (diagnostic builds): the 80-column wide class as before (A/B)
+  // The tail class (cmpc_tail.hip) takes 64 < n <= 72 at N <= 10 whatever the batch size (so a
+  // record gets the same kernel, and the same forces, in any batch). Its placement depends on the
+  // batch (measured on config-3 mixes, profiles/r05_j, r05_k; against the 80-column class for
+  // every n <= 80: 4096 -0.7 %, 16384 -4 %, 32768 -1.5 %, 65536 +4.4 %, 262144 +7 %):
+  //   1: on the handle's stream behind class 1, alone on the GPU once class 1 drains (from 131072
+  //      instances: +7 % at 262144 where beside class 1 gave +3 %);
+  //   2: first on its own side stream (side 2) beside class 1 (below 131072);
+  //   0: first on side 0 ahead of the 80-column class; 3: ahead of class 1 on the handle's stream.
+  // CMPC_TAIL=0 (diagnostic A/B builds): the 80-column wide class for every 64 < n <= 80.
+  // CMPC_T8_POS forces a placement.
+  static const int tail_env = diag_knob("CMPC_TAIL", 1);
+  const bool tail = tail_env != 0 && tail_class(P, 65);
+  const bool tail_on = tail && n_max > 64;
+  static const int t8_env = diag_knob("CMPC_T8_POS", -1);
+  const int t8_pos = (t8_env >= 0) ? t8_env : (batch >= 131072 ? 1 : 2);
+  // side streams forked and joined by this solve (the third only for the tail class's own chain)
+  const int nsides = (tail && t8_pos == 2) ? 3 : 2;
   bool cls_side_used = false;
   if (n_max > 64) {
     // From 16384 instances (and up to 4096) the classify pass runs on side 0 beside class 1 (which
@@ -140,12 +166,13 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       if ((e = hipStreamWaitEvent(ctx.side[0], ctx.fork, 0)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 63) / 64), dim3(64), 0, cs,
-                       d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr, c1_listed ? 1 : 0);
+                       d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr, c1_listed ? 1 : 0,
+                       tail ? 1 : 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     ctx.last_hdr = ctx.hdr;
     if (!CMPC_HDR_MEMSET) ctx.hdr ^= 1;
     if ((e = hipEventRecord(ctx.classified, cs)) != hipSuccess) return e;
-    for (int s = cls_side ? 1 : 0; s < kSideStreams; s++)
+    for (int s = cls_side ? 1 : 0; s < nsides; s++)
       if ((e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
     int grid_of[kLists];
     for (int j = 0; j < kLists; j++) grid_of[j] = batch;
@@ -168,6 +195,12 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     auto dq = [&](int lst, int lo, int hi) -> int* {
       return one_per_entry(lo, hi, P.N, batch) ? nullptr : &cnt[kDeq + lst];
     };
+    // the tail class first on side 0 / side 2 (t8_pos above); its hand-offs (list 10) go to the
+    // 80-column class on the handle's stream after the join (below)
+    if (tail && (t8_pos == 0 || t8_pos == 2) &&
+        (e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11],
+                         grid_of[9], ctx.side[t8_pos])) != hipSuccess)
+      return e;
     // the 64-wide class-1 build over its list (60 < n <= 64), ahead of the wide classes on side 1
     // (side 0 carries the 80 class, the longest chain at N = 10)
     if (split60 && (e = launch_class1(64, d_recs, batch, P, d_forces, d_status, d_iters, list[7],
@@ -176,8 +209,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // side 0: 80, 120, 144, 256; side 1: 96, 128, 192 (at N = 20 the 120-column class, which
     // carries the batch, runs beside the 128-column class)
     if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1],
-                             dq(0, 65, 80), grid_of[0],
-                             ctx.side[0])) != hipSuccess)
+                             dq(0, 65, 80), grid_of[0], ctx.side[0])) != hipSuccess)
       return e;
     if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], dq(1, 81, 96),
                                            grid_of[1], ctx.side[1])) != hipSuccess)
@@ -211,6 +243,12 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                                              grid_of[4], ctx.side[0])) != hipSuccess)
       return e;
   }
+  if (tail_on && t8_pos == 3) {  // the tail class ahead of class 1 on the handle's stream
+    if (cls_side_used && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
+    if ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11], batch,
+                         stream)) != hipSuccess)
+      return e;
+  }
   if (ev) (void)hipEventRecord(ev[0], stream);
   // class 1: up to N = 10 over the whole batch (it skips the instances above its row width
   // itself), from N = 11 over list 5
@@ -225,12 +263,23 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                       nullptr, batch, stream);
   }
   if (e != hipSuccess) return e;
+  if (tail_on && t8_pos == 1) {  // the tail class behind class 1 on the handle's stream
+    if (cls_side_used && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
+    if ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11], batch,
+                         stream)) != hipSuccess)
+      return e;
+  }
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (n_max > 64) {
-    for (int s = 0; s < kSideStreams; s++) {
+    for (int s = 0; s < nsides; s++) {
       if ((e = hipEventRecord(ctx.join[s], ctx.side[s])) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(stream, ctx.join[s], 0)) != hipSuccess) return e;
     }
+    // the tail classes' hand-offs (an active set past 64 positions) to the 80-column class: a
+    // small persistent grid, usually over an empty list
+    if (tail_on && (e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[10], &cnt[11],
+                                        &cnt[kDeq + 10], kHandoffGrid, stream)) != hipSuccess)
+      return e;
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
   return hipSuccess;
@@ -240,12 +289,19 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
 // record's gait table, the same test as the classify pass): exactly one kernel of the right
 // class, no classify pass, no side-stream fork/join. d_one = {1, 0}: a one-entry instance list.
 hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_forces,
-                         uint8_t* d_status, int32_t* d_iters, const int* d_one, hipStream_t stream) {
+                         uint8_t* d_status, int32_t* d_iters, const int* d_one, hipStream_t stream,
+                         bool allow_tail) {
   const int* cnt = d_one;
   const int* lst = d_one + 1;
   if (n <= 64)
     return launch_class1(n <= 60 ? 60 : 64, d_rec, 1, P, d_forces, d_status, d_iters, nullptr,
                          nullptr, nullptr, nullptr, 1, stream);
+  static const int tail_env = diag_knob("CMPC_TAIL", 1);
+  const bool in_tail = tail_env != 0 && tail_class(P, n);
+  if (allow_tail && in_tail)
+    return launch_tail(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, nullptr, 1, stream);
+  if (!allow_tail && in_tail)  // a tail-class hand-off: the form the batched launch uses
+    return launch_wide_w80_persist(d_rec, P, d_forces, d_status, d_iters, lst, cnt, nullptr, 1, stream);
   // the launch form the batched launch of this class would pick for a batch of one (one workgroup
   // per entry; the persistent form runs its loop once with deq == nullptr). Both forms round
   // alike (-ffp-contract=on, build.py): tests/test_gpu_parity.py::test_batch_size_invariance

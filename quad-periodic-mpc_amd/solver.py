@@ -98,7 +98,8 @@ def load_library(path: str = LIB_PATH):
     lib.cmpc_batch_stream.restype = ctypes.c_void_p
     lib.cmpc_last_error.restype = ctypes.c_char_p
     lib.cmpc_batch_enable_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    lib.cmpc_batch_enable_timing_every.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    if hasattr(lib, "cmpc_batch_enable_timing_every"):  # (A/B libraries built before round 4 lack it)
+        lib.cmpc_batch_enable_timing_every.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     lib.cmpc_batch_read_timing.argtypes = [ctypes.c_void_p, _fp, _ip, _ip]
     lib.cmpc_batch_estimate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
@@ -354,6 +355,11 @@ class BatchSolver:
         """Record HIP events around each size-class launch of the next ``steps`` solves (of every
         ``every``-th solve only, ``steps`` of them, when ``every`` > 1)."""
         self._timing_steps = int(steps)
+        if not hasattr(self.lib, "cmpc_batch_enable_timing_every"):
+            if every != 1:
+                raise CmpcError("this libcmpc_hip.so has no cmpc_batch_enable_timing_every")
+            _check(self.lib.cmpc_batch_enable_timing(self._h, int(steps)), "enable_timing")
+            return
         _check(self.lib.cmpc_batch_enable_timing_every(self._h, int(steps), int(every)), "enable_timing")
 
     def read_timing(self):

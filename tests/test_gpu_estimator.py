@@ -157,7 +157,8 @@ def test_config5_full_size_sampled_live_reference(cm, orc, solver_mod, on_stream
     assert (np.abs(fe_dev - fe_ref) / np.maximum(np.abs(fe_ref), 1.0)).max() <= 1e-5
     ok = st_ref == 0
     assert ok.mean() > 0.99
-    assert_parity(orc, rec_s, prm, forces.cpu().numpy()[idx], q_ref, ok, label="config 5 sampled")
+    assert_parity(orc, rec_s, prm, forces.cpu().numpy()[idx], q_ref, ok, label="config 5 sampled",
+                  gait="config5")
 
 
 @pytest.mark.parametrize("inst", [0, 7, 21])
@@ -195,7 +196,8 @@ def test_abi_estimator_sequence(cm, orc, inst, tmp_path):
         assert abs(d["static"][k, 3] - st) <= 1e-6 * max(1.0, abs(st))
     f = d["forces"].astype(np.float32)[None]
     if orc.ref_available():
+        # (one instance: the batch caps of the branch are checked by the batched tests)
         assert_parity(orc, g["final_records"][inst:inst + 1], prm, f, g["q_ref"][inst:inst + 1],
-                      label=f"ABI config 5 instance {inst}")
+                      label=f"ABI config 5 instance {inst}", cap=1.0)
     else:
         assert rel_force_err(f, g["q_ref"][inst:inst + 1]).max() <= 1e-4

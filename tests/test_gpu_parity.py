@@ -35,18 +35,55 @@ def tol_for(N):
 FP64_BRANCH_MIN_N = 11   # below this every instance is held to 1e-4 against qpOASES (the
                          # refinement's first horizon, CMPC_REFINE_FROM_N in cmpc_abi.cpp)
 FP64_BRANCH_TOL = 1e-5   # the fallback's bound against the fp64 optimum (measured <= 2.2e-6)
+# The fraction of a batch that may take the fp64-optimum branch, per (N, gait table): the rate
+# measured on the live and golden cases plus a margin (profiles/r05_*/pytest.log prints every
+# case's count). A regression that pushes more instances past 1e-4 of qpOASES fails here even when
+# each of them stays within 1e-5 of the optimum. All-stance tables at N = 20 are where the
+# reference drifts most (about 14 % of them beyond 1e-4 of the optimum).
+FP64_BRANCH_CAP = {(20, "standing"): 0.16, (16, "standing"): 0.005}
+FP64_BRANCH_CAP_DEFAULT = 0.02
 
 
-def assert_parity(orc, recs, prm, f, q_ref, ok=None, label=""):
+def branch_cap(N, gait):
+    if N < FP64_BRANCH_MIN_N:
+        return 0.0
+    return FP64_BRANCH_CAP.get((N, gait), FP64_BRANCH_CAP_DEFAULT)
+
+
+def assert_failed_reference(orc, recs, prm, f, st, st_ref, label=""):
+    """The instances where the reference's qpOASES fails (nWSR = 100 exhausted, st_ref != 0) are
+    checked against the float64 optimum of the same QP (oracle.fp64_solve, nWSR 1000) instead of
+    being dropped: ours must have solved them and be within FP64_BRANCH_TOL of it."""
+    idx = np.nonzero(st_ref != 0)[0]
+    for i in idx:
+        x64, ri = orc.fp64_solve(recs[i], prm)
+        if ri != 0:
+            print(f"[parity] {label}: instance {i}: qpOASES fails in fp64 too (ret {ri}), skipped")
+            continue
+        e = np.abs(f[i] - x64).max() / max(np.abs(x64).max(), 1.0)
+        print(f"[parity] {label}: instance {i} (reference qpOASES ret {st_ref[i]}): ours vs the fp64 "
+              f"optimum {e:.2e}, status {st[i]}")
+        assert st[i] == 0 and e <= FP64_BRANCH_TOL, (i, st[i], e)
+    return len(idx)
+
+
+def assert_parity(orc, recs, prm, f, q_ref, ok=None, label="", gait="trotting", cap=None):
     """err vs qpOASES <= 1e-4; from N = 11, err vs the fp64 optimum <= 1e-5 instead (module
-    doc). Prints how many instances took that branch and how far the reference is from the
-    optimum on them."""
+    doc), for at most branch_cap(N, gait) of the batch. Prints how many instances took that branch
+    and how far the reference is from the optimum on them."""
     ok = np.ones(len(q_ref), bool) if ok is None else ok
     err = rel_force_err(f[ok], q_ref[ok])
     bad = np.nonzero(err > tol_for(prm.horizon))[0]
     msg = (f"[parity] {label} N={prm.horizon}: {len(err)} instances, max err vs qpOASES "
            f"{err.max():.2e}, {len(bad)} beyond {tol_for(prm.horizon):.0e}")
+    cap = branch_cap(prm.horizon, gait) if cap is None else cap
     if len(bad) and prm.horizon >= FP64_BRANCH_MIN_N:
+        print(msg + f" ({100 * len(bad) / len(err):.2f} % of the batch take the fp64 branch, cap "
+              f"{100 * cap:.1f} %)")
+        # the cap as a rate: at most cap * m + 3 binomial standard deviations of m instances (so a
+        # handful of golden instances may hold one, a 2048-instance sample only the measured rate)
+        allowed = cap * len(err) + 3.0 * np.sqrt(len(err) * cap * (1.0 - cap))
+        assert len(bad) <= allowed, (len(bad), len(err), cap, allowed)
         idx = np.nonzero(ok)[0][bad]
         q_ok = q_ref[ok]
         e64s, eref = [], []
@@ -95,11 +132,22 @@ def test_forces_match_qpoases_golden(cm, orc, solver_mod, name):
         print(f"[golden] {name}: max err vs qpOASES {err.max():.2e}")
         assert err.max() <= tol_for(prm.horizon), (name, err.max(), int(err.argmax()))
     else:
-        assert_parity(orc, g["records"], prm, f, g["q_ref"], ok, label=f"golden {name}")
+        gait = "standing" if ("standing" in name or "allstance" in name) else \
+            ("walking" if "walking" in name else "trotting")
+        assert_parity(orc, g["records"], prm, f, g["q_ref"], ok, label=f"golden {name}", gait=gait)
 
 
-@pytest.mark.parametrize("name", ["n10_mixed", "n10_edge"])
-def test_condensation_matches_golden(cm, solver_mod, name):
+# qH / qg of the structured condensation (cmpc_condense.hip) against the reference's dense fp32
+# GEMMs (the golden qH / qg, SolverMPC.cpp:806-814) and against the float64 condensation
+# (oracle.fp64_condense), normwise: max |difference| / max |qH| (qg likewise). The reference's own
+# fp32 qH is 2.2e-7 .. 5.5e-7 from the fp64 one on these fixtures (N = 10 .. 20), so the force
+# differences of up to ~1e-4 at N >= 16 (FP64_BRANCH_MIN_N) come from the conditioning of the QP,
+# not from a drift of the condensed matrices.
+COND_BOUND = {10: 2e-6, 12: 2e-6, 16: 3e-6, 20: 4e-6}
+
+
+@pytest.mark.parametrize("name", ["n10_mixed", "n10_edge", "n12_allstance", "n16_standing", "n20_trot"])
+def test_condensation_matches_golden(cm, orc, solver_mod, name):
     import torch
     g = load_golden(name)
     prm = golden_params(cm, g)
@@ -112,11 +160,19 @@ def test_condensation_matches_golden(cm, solver_mod, name):
     s.condense(recs, H, gg)
     torch.cuda.synchronize()
     H = H.cpu().numpy(); gg = gg.cpu().numpy()
+    bound = COND_BOUND[N]
     for i in range(k):
-        scale = np.abs(g["qH"][i]).max()
-        assert np.abs(H[i] - g["qH"][i]).max() <= 2e-6 * scale
-        gs = np.abs(g["qg"][i]).max()
-        assert np.abs(gg[i] - g["qg"][i]).max() <= 2e-6 * gs
+        H64, g64 = orc.fp64_condense(g["records"][i], prm)
+        scale, gs = np.abs(H64).max(), np.abs(g64).max()
+        e_ref = np.abs(H[i] - g["qH"][i]).max() / scale
+        eg_ref = np.abs(gg[i] - g["qg"][i]).max() / gs
+        e64 = np.abs(H[i] - H64).max() / scale
+        eg64 = np.abs(gg[i] - g64).max() / gs
+        e_ref64 = np.abs(g["qH"][i] - H64).max() / scale
+        print(f"[condense] {name} #{i}: qH vs reference {e_ref:.2e}, vs fp64 {e64:.2e} (reference vs "
+              f"fp64 {e_ref64:.2e}); qg vs reference {eg_ref:.2e}, vs fp64 {eg64:.2e}")
+        assert max(e_ref, eg_ref) <= bound, (e_ref, eg_ref)
+        assert max(e64, eg64) <= bound, (e64, eg64)
 
 
 def test_edge_cases(cm, solver_mod):
@@ -158,7 +214,8 @@ def test_random_batches_match_reference_live(cm, orc, solver_mod, N, stress, fra
     print(f"[live] N={N} {gait} stress={stress} frac={frac}: n {n.min()}..{n.max()}, "
           f"qpOASES solved {ok.sum()} of {B}")
     assert (st[ok] == 0).all(), np.bincount(st[ok])
-    assert_parity(orc, recs, prm, f, q, ok, label=f"live {gait} stress={stress} frac={frac}")
+    assert_parity(orc, recs, prm, f, q, ok, label=f"live {gait} stress={stress} frac={frac}", gait=gait)
+    assert_failed_reference(orc, recs, prm, f, st, st_ref, label=f"live N={N} {gait}")
 
 
 @pytest.mark.parametrize("gait", ["standing", "walking", "trotting"])
@@ -176,9 +233,9 @@ def test_deployed_horizon_large_sample_live(cm, orc, solver_mod, gait):
     f, st, _ = gpu_solve(solver_mod, prm, recs)
     ok = st_ref == 0
     assert (st[ok] == 0).all(), np.bincount(st[ok])
-    err = rel_force_err(f[ok], q[ok])
-    assert (err > tol_for(N)).mean() <= 0.02, (err > tol_for(N)).sum()
-    assert_parity(orc, recs, prm, f, q, ok, label=f"N=16 {gait} x{B}")
+    assert_parity(orc, recs, prm, f, q, ok, label=f"N=16 {gait} x{B}", gait=gait)
+    nf = assert_failed_reference(orc, recs, prm, f, st, st_ref, label=f"N=16 {gait} x{B}")
+    print(f"[parity] N=16 {gait} x{B}: {nf} instances where the reference's qpOASES fails")
 
 
 CLASS_EDGES = [0, 60, 64, 80, 96, 120, 128, 144, 192, 256]  # class 1 (60 / 64 builds), wide 80 .. 256
