@@ -12,7 +12,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <mutex>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -54,6 +56,7 @@ struct cmpc_batch {
   float* h_pin = nullptr;
   // side streams + fork/join events for the wider size classes (cmpc_launch.hip)
   cmpc::LaunchCtx ctx;
+  bool pooled_sides = false;     // ctx.side came from the process-wide pool (acquire_sides)
   // optional per-launch timing (cmpc_batch_enable_timing)
   std::vector<hipEvent_t> ev;
   int ev_steps = 0, ev_next = 0;
@@ -63,6 +66,58 @@ struct cmpc_batch {
 #ifndef CMPC_REFINE_FROM_N
 #define CMPC_REFINE_FROM_N 11  // first horizon whose wide classes refine (diagnostic builds move it)
 #endif
+
+// Side streams come from a process-wide pool and go back to it when a handle is destroyed; a new
+// handle takes the oldest free set. The runtime maps streams onto a few hardware queues
+// (GPU_MAX_HW_QUEUES = 4 by default) as they are created, and a set created while other streams
+// were alive can share a hardware queue with the caller's stream: its side classes then queue
+// behind class 1 (32768 instances 0.90 -> 1.17-1.25 ms per solve, 65536 1.48 -> 1.83 ms;
+// scripts/stream_probe.py, profiles/r05_ab/r05_q .. r05_t). With the oldest free set first, one
+// handle at a time always runs on the first handle's streams. Pooled per device.
+namespace {
+struct SideSet {
+  int dev;
+  bool busy;
+  std::array<hipStream_t, cmpc::kSideStreams> s;
+};
+struct SidePool {
+  std::mutex mu;
+  std::vector<SideSet> sets;  // in creation order
+};
+SidePool& side_pool() {
+  static SidePool* p = new SidePool();  // never destroyed: the streams live as long as the process
+  return *p;
+}
+hipError_t acquire_sides(std::array<hipStream_t, cmpc::kSideStreams>& out, int prio) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(side_pool().mu);
+  for (auto& set : side_pool().sets) {
+    if (set.dev == dev && !set.busy) {
+      set.busy = true;
+      out = set.s;
+      return hipSuccess;
+    }
+  }
+  SideSet set{dev, true, {}};
+  for (int j = 0; j < cmpc::kSideStreams; j++) {
+    e = hipStreamCreateWithPriority(&set.s[j], hipStreamNonBlocking, prio);
+    if (e != hipSuccess) {
+      for (int k = 0; k < j; k++) (void)hipStreamDestroy(set.s[k]);
+      return e;
+    }
+  }
+  side_pool().sets.push_back(set);
+  out = set.s;
+  return hipSuccess;
+}
+void release_sides(const std::array<hipStream_t, cmpc::kSideStreams>& s) {
+  std::lock_guard<std::mutex> lk(side_pool().mu);
+  for (auto& set : side_pool().sets)
+    if (set.s[0] == s[0]) set.busy = false;
+}
+}  // namespace
 
 static cmpc::KParams make_kparams(const cmpc_params& p) {
   cmpc::KParams k{};
@@ -156,10 +211,16 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (cmpc::diag_knob("CMPC_SIDE_PRIORITY", 1) == 0) prio_hi = prio_lo;
-  for (int j = 0; j < cmpc::kSideStreams; j++) {
-    e = hipStreamCreateWithPriority(&h->ctx.side[j], hipStreamNonBlocking, prio_hi);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.join[j], hipEventDisableTiming);
+  {
+    std::array<hipStream_t, cmpc::kSideStreams> sides{};
+    e = acquire_sides(sides, prio_hi);
     if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("side streams", e); }
+    for (int j = 0; j < cmpc::kSideStreams; j++) h->ctx.side[j] = sides[j];
+    h->pooled_sides = true;
+  }
+  for (int j = 0; j < cmpc::kSideStreams; j++) {
+    e = hipEventCreateWithFlags(&h->ctx.join[j], hipEventDisableTiming);
+    if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("side events", e); }
   }
   e = hipEventCreateWithFlags(&h->ctx.fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.classified, hipEventDisableTiming);
@@ -188,10 +249,17 @@ extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
   if (h->d_admm_slabs) (void)hipFree(h->d_admm_slabs);
   free_staging(h);
   for (auto e : h->ev) (void)hipEventDestroy(e);
-  for (int j = 0; j < cmpc::kSideStreams; j++) {
-    if (h->ctx.side[j]) (void)hipStreamDestroy(h->ctx.side[j]);
-    if (h->ctx.join[j]) (void)hipEventDestroy(h->ctx.join[j]);
+  if (h->pooled_sides) {
+    // back to the pool once every side stream is idle (the next handle may fork on them at once)
+    std::array<hipStream_t, cmpc::kSideStreams> sides{};
+    for (int j = 0; j < cmpc::kSideStreams; j++) {
+      sides[j] = h->ctx.side[j];
+      (void)hipStreamSynchronize(sides[j]);
+    }
+    release_sides(sides);
   }
+  for (int j = 0; j < cmpc::kSideStreams; j++)
+    if (h->ctx.join[j]) (void)hipEventDestroy(h->ctx.join[j]);
   if (h->ctx.fork) (void)hipEventDestroy(h->ctx.fork);
   if (h->ctx.classified) (void)hipEventDestroy(h->ctx.classified);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);

@@ -45,9 +45,38 @@ def main():
     def fresh(label):
         s = sm.BatchSolver(prm, max_batch=B, stream=torch.cuda.current_stream())
         t = timeit(lambda: s.solve(recs, f, st))
+        s.enable_timing(10)
+        for _ in range(10):
+            s.solve(recs, f, st)
+        ms, _ = s.read_timing()
         s.close()
+        print(f"{label:40s} {t:.4f} ms  (class 1 {ms[:, 0].mean():.4f}, beyond it {ms[:, 1].mean():.4f})",
+              flush=True)
+
+    def piped(label):
+        pipe = par.RootPipeline(prm, B, chunks=1, device="cuda")
+        t = timeit(lambda: pipe.step(recs))
+        pipe.close()
         print(f"{label:40s} {t:.4f} ms", flush=True)
 
+    if os.environ.get("PROBE_ORDER") == "model":  # the scaling model's pieces, twice
+        recs_all = torch.from_numpy(cm.make_instances(262144, N)).cuda()
+        for rep in range(2):
+            for G in (1, 2, 4, 8):
+                local = 262144 // G
+                pipe = par.RootPipeline(prm, local, chunks=par.auto_chunks(local, G), device="cuda")
+                t = timeit(lambda: pipe.step(recs_all[:local]))
+                pipe.close()
+                print(f"rep {rep} G={G}: {local} in {len(pipe.sizes)} pieces {t:.4f} ms", flush=True)
+        return
+    if os.environ.get("PROBE_ORDER") == "pipe_first":
+        piped("RootPipeline first")
+        fresh("fresh after it")
+        time.sleep(5)
+        fresh("fresh after 5 s idle")
+        piped("RootPipeline again")
+        fresh("fresh again")
+        return
     fresh("fresh handle")
     for k in range(6):  # handles of other sizes, created and destroyed
         s = sm.BatchSolver(prm, max_batch=4096 * (k + 1))
