@@ -78,9 +78,9 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
 // (Round 4: only the class holding 6 N itself one-per-entry measured -0.3 % at config 3; the same
 // with the 80 class kept one-per-entry at N <= 10, i.e. the 128 class persistent at N = 20 and
 // the 120 class at N = 16, -1.0 % at config 5, +0.3 % at N = 16, profiles/r04_ab/r04_t*.)
-// workgroups of the 80-column class's persistent launch over the tail classes' hand-offs (an
-// active set past 64 positions: none in any measured workload)
-constexpr int kHandoffGrid = 16;
+// workgroups of the 80-column class's persistent launch over the tail class's hand-offs (an
+// active set past 64 positions: none in any measured workload; one workgroup solves them in turn)
+constexpr int kHandoffGrid = 1;
 
 bool one_per_entry(int lo, int hi, int N, int batch) {
   static const int form = diag_knob("CMPC_WIDE_FORM", 0);
@@ -145,6 +145,12 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   const int t8_pos = (t8_env >= 0) ? t8_env : (batch >= 131072 ? 1 : 2);
   // side streams forked and joined by this solve (the third only for the tail class's own chain)
   const int nsides = (tail && t8_pos == 2) ? 3 : 2;
+  // the tail class's hand-offs, behind it on its stream: a one-workgroup persistent launch of the
+  // 80-column class (it reads the final count once the tail class is done)
+  auto launch_handoff = [&](hipStream_t s) -> hipError_t {
+    return launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[10], &cnt[11], &cnt[kDeq + 10],
+                           kHandoffGrid, s);
+  };
   bool cls_side_used = false;
   if (n_max > 64) {
     // From 16384 instances (and up to 4096) the classify pass runs on side 0 beside class 1 (which
@@ -195,12 +201,22 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     auto dq = [&](int lst, int lo, int hi) -> int* {
       return one_per_entry(lo, hi, P.N, batch) ? nullptr : &cnt[kDeq + lst];
     };
-    // the tail class first on side 0 / side 2 (t8_pos above); its hand-offs (list 10) go to the
-    // 80-column class on the handle's stream after the join (below)
+    // the tail class first on side 0 / side 2 (t8_pos above), its hand-offs (list 10) to the
+    // 80-column class right behind it on the same stream
     if (tail && (t8_pos == 0 || t8_pos == 2) &&
-        (e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11],
-                         grid_of[9], ctx.side[t8_pos])) != hipSuccess)
+        ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11],
+                          grid_of[9], ctx.side[t8_pos])) != hipSuccess ||
+         (e = launch_handoff(ctx.side[t8_pos])) != hipSuccess))
       return e;
+    // CMPC_W96_FIRST (diagnostic A/B): the 96-column class ahead of the 64-wide class-1 build on
+    // side 1 (its few long solves start at once instead of behind that build)
+    static const int w96_first = diag_knob("CMPC_W96_FIRST", 0);
+    auto launch_w96 = [&]() -> hipError_t {
+      return n_max > 80 ? launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], dq(1, 81, 96),
+                                          grid_of[1], ctx.side[1])
+                        : hipSuccess;
+    };
+    if (w96_first && (e = launch_w96()) != hipSuccess) return e;
     // the 64-wide class-1 build over its list (60 < n <= 64), ahead of the wide classes on side 1
     // (side 0 carries the 80 class, the longest chain at N = 10)
     if (split60 && (e = launch_class1(64, d_recs, batch, P, d_forces, d_status, d_iters, list[7],
@@ -211,9 +227,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1],
                              dq(0, 65, 80), grid_of[0], ctx.side[0])) != hipSuccess)
       return e;
-    if (n_max > 80 && (e = launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], dq(1, 81, 96),
-                                           grid_of[1], ctx.side[1])) != hipSuccess)
-      return e;
+    if (!w96_first && (e = launch_w96()) != hipSuccess) return e;
     // the 120-column build on side 0 from N = 14 (every trot instance at N = 17..20, beside the
     // 96-column trot class at N = 14..16); below, on side 1 behind the sparse 96 class: at N = 10
     // its launch (few or no instances) otherwise lengthens side 0's 80-class chain, the step's
@@ -246,7 +260,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   if (tail_on && t8_pos == 3) {  // the tail class ahead of class 1 on the handle's stream
     if (cls_side_used && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
     if ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11], batch,
-                         stream)) != hipSuccess)
+                         stream)) != hipSuccess ||
+        (e = launch_handoff(stream)) != hipSuccess)
       return e;
   }
   if (ev) (void)hipEventRecord(ev[0], stream);
@@ -266,7 +281,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   if (tail_on && t8_pos == 1) {  // the tail class behind class 1 on the handle's stream
     if (cls_side_used && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
     if ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11], batch,
-                         stream)) != hipSuccess)
+                         stream)) != hipSuccess ||
+        (e = launch_handoff(stream)) != hipSuccess)
       return e;
   }
   if (ev) (void)hipEventRecord(ev[1], stream);
@@ -275,11 +291,6 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       if ((e = hipEventRecord(ctx.join[s], ctx.side[s])) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(stream, ctx.join[s], 0)) != hipSuccess) return e;
     }
-    // the tail classes' hand-offs (an active set past 64 positions) to the 80-column class: a
-    // small persistent grid, usually over an empty list
-    if (tail_on && (e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[10], &cnt[11],
-                                        &cnt[kDeq + 10], kHandoffGrid, stream)) != hipSuccess)
-      return e;
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
   return hipSuccess;
