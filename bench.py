@@ -391,8 +391,8 @@ def scaling_model(args, cm, dev, sync):
     out_b = 4 * 12 * N
     recs_all = torch.from_numpy(cm.make_instances(G_total, N, random_contact_frac=args.random_contact_frac)).to(dev)
     rows, t1 = [], None
-    def timed_pieces(local, chunks):
-        pipe = par.RootPipeline(prm, local, chunks=chunks, device=dev)
+    def timed_pieces(local, chunks, out_steps=0):
+        pipe = par.RootPipeline(prm, local, chunks=chunks, device=dev, out_steps=out_steps)
         recs = recs_all[:local]
         for _ in range(3):
             pipe.step(recs)
@@ -430,6 +430,20 @@ def scaling_model(args, cm, dev, sync):
                 row["speedup" + key] = round(t1 / t, 3)
             row["xgmi_mb_root_sends"] = round((G - 1) * local * rec_b / 1e6, 2)
             row["xgmi_mb_root_receives"] = round((G - 1) * local * out_b / 1e6, 2)
+        # the same with the step-0 forces only (cmpc_batch_set_output_steps(1): what a caller of
+        # get_solution(0..11) reads, ConvexMPCLocomotion.cpp:832-845): 48 B gathered per instance
+        t0s, _ = timed_pieces(local, par.auto_chunks(local, G), out_steps=1)
+        row["step0_t_solve_ms_measured"] = round(t0s * 1e3, 4)
+        if G == 1:
+            t1s = t0s
+            row["step0_speedup"] = 1.0
+        else:
+            sc = [p * rec_b / (XGMI_LINK_GBS * 1e9) for p in pieces]
+            ga = [p * 48 / (XGMI_LINK_GBS * 1e9) for p in pieces]
+            inner = sum(sc[1:]) + sum(ga[:-1])
+            t = t0s + sc[0] + ga[-1] + max(0.0, inner - t0s)
+            row["step0_t_model_ms"] = round(t * 1e3, 4)
+            row["step0_speedup"] = round(t1s / t, 3)
         rows.append(row)
     del recs_all
     return {"kind": "model (not a measurement): per-rank solve times measured on this GPU, "

@@ -213,6 +213,11 @@ CMPC_EXTERNC void cmpc_batch_destroy(cmpc_batch* h);
  * (may be NULL). Asynchronous on the handle's stream. Returns 0 or a negative error. */
 CMPC_EXTERNC int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int batch,
                                   float* d_forces, uint8_t* d_status, int32_t* d_iters);
+/* Forces kept per instance: the first `steps` horizon steps (12 x steps floats per instance,
+ * stride of d_forces / forces of the two solves below and of cmpc_batch_rollout), 0 = every step
+ * (12N, the default). A caller that reads only get_solution(0..11) as ConvexMPCLocomotion.cpp:
+ * 832-845 does can keep step 0 (48 B instead of 480 B per instance at N = 10). New API. */
+CMPC_EXTERNC int cmpc_batch_set_output_steps(cmpc_batch* h, int steps);
 /* Same, host buffers in and out (H2D + solve + D2H on the handle's stream, synchronous). */
 CMPC_EXTERNC int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int batch,
                                        float* forces, uint8_t* status, int32_t* iters);

@@ -33,6 +33,7 @@ int fail(const char* what, hipError_t e) {
 struct cmpc_batch {
   cmpc_params prm;
   cmpc::KParams kp;
+  int out_steps = 0;             // cmpc_batch_set_output_steps (0: every step)
   int max_batch = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -135,6 +136,7 @@ static cmpc::KParams make_kparams(const cmpc_params& p) {
   k.dt64 = (double)k.dt;
   k.dth64 = 0.5 * k.dt64 * k.dt64;
   k.dt3_64 = k.dt64 * k.dt64 * k.dt64 / 6.0;
+  k.out_cols = 12 * p.horizon;
   return k;
 }
 
@@ -186,7 +188,18 @@ extern "C" int cmpc_batch_set_params(cmpc_batch* h, const cmpc_params* prm) {
   }
   h->prm = *prm;
   h->kp = make_kparams(*prm);
+  if (h->out_steps > 0 && h->out_steps < prm->horizon) h->kp.out_cols = 12 * h->out_steps;
   return ensure_admm_slabs(h);
+}
+
+extern "C" int cmpc_batch_set_output_steps(cmpc_batch* h, int steps) {
+  if (!h || steps < 0) {
+    g_last_error = "cmpc_batch_set_output_steps: bad arguments";
+    return -1;
+  }
+  h->out_steps = steps;
+  h->kp.out_cols = 12 * ((steps > 0 && steps < h->prm.horizon) ? steps : h->prm.horizon);
+  return 0;
 }
 
 extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int max_batch,
@@ -311,7 +324,7 @@ extern "C" int cmpc_batch_assemble(cmpc_batch* h, float* d_loco, const cmpc_loco
   }
   cmpc::LocoParams kp{lp->dt,        lp->iters_between_mpc, lp->x_drag_gain,  h->kp.N,
                       h->kp.rec_words, lp->hip_x,            lp->hip_y,        lp->abad_link,
-                      lp->swing_height, lp->bonus_swing};
+                      lp->swing_height, lp->bonus_swing,     h->kp.out_cols};
   hipError_t e = cmpc::launch_assemble(d_loco, kp, d_records, d_due, batch, h->stream);
   if (e != hipSuccess) return fail("launch_assemble", e);
   return 0;
@@ -324,7 +337,7 @@ extern "C" int cmpc_batch_rollout(cmpc_batch* h, float* d_loco, const float* d_r
     g_last_error = "cmpc_batch_rollout: bad arguments";
     return -1;
   }
-  cmpc::LocoParams kp{h->kp.dt, 1, 0.f, h->kp.N, h->kp.rec_words, 0.f, 0.f, 0.f, 0.f, 0.f};
+  cmpc::LocoParams kp{h->kp.dt, 1, 0.f, h->kp.N, h->kp.rec_words, 0.f, 0.f, 0.f, 0.f, 0.f, h->kp.out_cols};
   hipError_t e = cmpc::launch_rollout(d_loco, d_records, d_forces, d_xi6, d_due, kp, h->kp.dt,
                                       batch, h->stream);
   if (e != hipSuccess) return fail("launch_rollout", e);
@@ -499,7 +512,7 @@ static int solve_single_host(cmpc_batch* h, const float* record, float* forces, 
     return fail("D2H", e);
   if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail("sync", e);
   if (int r = single_handoff(h, n, pin_out, N, iters)) return r;
-  std::memcpy(forces, pin_out, 12 * N * sizeof(float));
+  std::memcpy(forces, pin_out, h->kp.out_cols * sizeof(float));
   if (status) std::memcpy(status, pin_out + 12 * N, 1);
   return 0;
 }
@@ -518,7 +531,8 @@ extern "C" int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int ba
   if ((e = hipMemcpyAsync(h->d_rec, records, rw * batch * sizeof(float), hipMemcpyHostToDevice, h->stream)) != hipSuccess)
     return fail("H2D", e);
   if (int r = cmpc_batch_solve(h, h->d_rec, batch, h->d_forces, h->d_status, h->d_iters)) return r;
-  if ((e = hipMemcpyAsync(forces, h->d_forces, sizeof(float) * 12 * N * batch, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(forces, h->d_forces, sizeof(float) * h->kp.out_cols * batch, hipMemcpyDeviceToHost,
+                          h->stream)) != hipSuccess)
     return fail("D2H", e);
   if (status && (e = hipMemcpyAsync(status, h->d_status, batch, hipMemcpyDeviceToHost, h->stream)) != hipSuccess)
     return fail("D2H", e);

@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void cmpc_rollout_kernel(float* __restrict__ l
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= batch || (due && !due[i])) return;
   const float* rec = recs + (size_t)i * lp.rec_words;
-  const float* u = forces + (size_t)i * 12 * lp.horizon;  // step 0: 12 forces, leg * 3 + axis
+  const float* u = forces + (size_t)i * lp.out_cols;  // step 0: 12 forces, leg * 3 + axis
   Model md;
   make_model(rec, dt, md);
   float BdtT[12][16];

@@ -834,7 +834,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   lsync();
   if (ok && v < n) sh.P[12 * sh.varblk[v] + sh.varcol[v]] = xv;
   lsync();
-  for (int t = 4 * v; t < 12 * N; t += 256)
+  for (int t = 4 * v; t < P.out_cols; t += 256)  // (the leading steps kept, 12 N by default)
     *reinterpret_cast<float4*>(&fout[t]) = *reinterpret_cast<const float4*>(&sh.P[t]);
   if (v == 0) {
     st_out[0] = (uint8_t)status;
@@ -873,7 +873,7 @@ __global__ __launch_bounds__(64, NV == 60 ? CMPC_W1_WAVES_60 : CMPC_W1_WAVES_PER
   const unsigned hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
   const unsigned xcc_id = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
 #endif
-  solve_c1<NV>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * 12 * P.N, status + t,
+  solve_c1<NV>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * P.out_cols, status + t,
                iters ? iters + t : nullptr, ovf_list, ovf_count, t);
 #ifdef CMPC_PLACE_PROF
   const unsigned long long t_end = wall_clock64();

@@ -86,6 +86,9 @@ __device__ void condense_one(const float* __restrict__ rec, const KParams& P, Sh
         for (int j = 0; j < 13; j++) bw[j] = sh.BdtT[w - 12 * i][j];
         float val = 2.f * dot13(bw, z);
         if (w == v) val += P.alpha2;  // qH = 2 (B'SB + alpha I), SolverMPC.cpp:806
+#ifdef CMPC_DIAG_PERTURB  // diagnostic builds only: a deliberately wrong qH (shows the parity gate fails)
+        val *= 1.f + CMPC_DIAG_PERTURB;
+#endif
         H[(size_t)v * n + w] = val;
         H[(size_t)w * n + v] = val;
       }

@@ -32,6 +32,8 @@ struct KParams {
   int rec_words;
   int max_iter;    // active-set cap; the kernels allow max_iter + 2 n
   int refine;      // wide classes: one fp64 refinement step of the converged active set (N > 10)
+  int out_cols;    // forces written per instance: 12 x the leading horizon steps kept
+                   // (cmpc_batch_set_output_steps; 12 N by default)
   // the step's fp64 powers for that refinement (scalar registers, not per-lane conversions)
   double dt64, dth64, dt3_64;  // dt, dt^2 / 2, dt^3 / 6
 };
@@ -44,6 +46,7 @@ struct LocoParams {
   int horizon;
   int rec_words;
   float hip_x, hip_y, abad_link, swing_height, bonus_swing;  // foot placement (cmpc_loco_params)
+  int out_cols;    // rollout: the forces' stride (the handle's KParams::out_cols)
 };
 
 // Scratch ints needed by launch_solve for max_batch instances.

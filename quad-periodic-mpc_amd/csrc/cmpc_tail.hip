@@ -946,7 +946,7 @@ __device__ __forceinline__ void solve_t(const float* __restrict__ rec, const KPa
   if (ok) sh.P[12 * sh.varblk[v] + sh.varcol[v]] = xv;
   if (ok && ts == 0 && 64 + ti < n) sh.P[12 * sh.varblk[64 + ti] + sh.varcol[64 + ti]] = xt;
   tsync();
-  for (int t = 4 * v; t < 12 * N; t += 256)
+  for (int t = 4 * v; t < P.out_cols; t += 256)  // (the leading steps kept, 12 N by default)
     *reinterpret_cast<float4*>(&fout[t]) = *reinterpret_cast<const float4*>(&sh.P[t]);
   if (v == 0) {
     st_out[0] = (uint8_t)status;
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(64, CMPC_TAIL_WAVES_PER_EU) void cmpc_solve_t_kerne
   const int b = blockIdx.x;
   if (b >= *in_count) return;
   const int t = in_list[b];
-  solve_t<kTailRows>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * 12 * P.N, status + t,
+  solve_t<kTailRows>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * P.out_cols, status + t,
                      iters ? iters + t : nullptr, ovf_list, ovf_count, t);
 }
 

@@ -1432,7 +1432,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     wbar();
     if (ok && h == 0 && r < n) sh.P[12 * sh.varblk[r] + sh.varcol[r]] = xv;
     wbar();
-    for (int i = 4 * t; i < 12 * N; i += 4 * G::NT)
+    for (int i = 4 * t; i < P.out_cols; i += 4 * G::NT)  // (the leading steps kept, 12 N by default)
       *reinterpret_cast<float4*>(&fout[i]) = *reinterpret_cast<const float4*>(&sh.P[i]);
     if (t == 0) {
       st_out[0] = (uint8_t)status;
@@ -1492,7 +1492,7 @@ __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGP
     const int b = blockIdx.x;
     if (b >= count) return;
     const int inst = A.in_list[b];
-    solve_w<NV, REFINE>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
+    solve_w<NV, REFINE>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * A.P.out_cols,
                         A.status + inst, A.iters ? A.iters + inst : nullptr);
   } else {
     for (int round = 0;; round++) {
@@ -1502,7 +1502,7 @@ __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGP
       const int b = __builtin_amdgcn_readfirstlane(sh.deq_b);
       if (b >= count) break;
       const int inst = A.in_list[b];
-      solve_w<NV, REFINE>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * 12 * A.P.N,
+      solve_w<NV, REFINE>(A.recs + (size_t)inst * A.P.rec_words, A.P, sh, A.forces + (size_t)inst * A.P.out_cols,
                           A.status + inst, A.iters ? A.iters + inst : nullptr);
       wbar();  // every wave is done with this instance's LDS before the next record lands there
     }

@@ -210,7 +210,7 @@ class RootPipeline:
 
     def __init__(self, params, global_batch: int, chunks: Optional[int] = None, *, group=None,
                  device=None, src: int = 0, solve_fn=None, record_words: Optional[int] = None,
-                 lanes: Optional[int] = None):
+                 lanes: Optional[int] = None, out_steps: int = 0):
         from .records import record_words as _rw
         self.params = params
         self.N = params.horizon
@@ -227,7 +227,11 @@ class RootPipeline:
         self.local_batch = self.stop - self.start
         self.device = device
         dev = device
-        cols = 12 * self.N
+        # forces kept per instance: every step (12 N) or, with out_steps, the leading steps only
+        # (cmpc_batch_set_output_steps: a caller of get_solution(0..11) gathers 48 B, not 480 B)
+        self.out_steps = int(out_steps) if 0 < int(out_steps) < self.N else 0
+        cols = 12 * (self.out_steps or self.N)
+        self.cols = cols
         # this rank's rows: records in, forces / status out (chunk c = rows of plan[rank][c])
         self._last_root = None
         # at world 1 the records are solved where they lie (no local copy)
@@ -269,6 +273,9 @@ class RootPipeline:
                 self._streams = [torch.cuda.Stream(dev) for _ in range(nl)]
                 self._solvers = [solver_mod.BatchSolver(params, max_batch=max(1, max(self.sizes)), stream=st)
                                  for st in self._streams]
+            for sv in self._solvers:
+                if self.out_steps:
+                    sv.set_output_steps(self.out_steps)
             self._solver = self._solvers[0]
 
     def _lane(self, c):

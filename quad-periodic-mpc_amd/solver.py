@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = (
     "update_problem_data_floats", "_Z13update_x_dragf", "f_ext", "simulation_time",
     "f_est", "f_est_smoothed", "f_est_static",
     "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
-    "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_condense", "cmpc_batch_stream",
+    "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_set_output_steps", "cmpc_batch_condense",
+    "cmpc_batch_stream",
     "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_enable_timing_every", "cmpc_batch_read_timing", "cmpc_batch_estimate",
     "cmpc_batch_assemble", "cmpc_batch_rollout", "cmpc_batch_admm",
     "cmpc_batch_quadprog",   # include/cmpc_quadprog.h
@@ -89,6 +90,7 @@ def load_library(path: str = LIB_PATH):
     lib.cmpc_batch_solve.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.cmpc_batch_solve_host.argtypes = [ctypes.c_void_p, _fp, ctypes.c_int, _fp, _u8p, _ip]
+    lib.cmpc_batch_set_output_steps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.cmpc_batch_condense.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p]
     lib.cmpc_batch_admm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -228,6 +230,18 @@ class BatchSolver:
         return self.params.horizon
 
     @property
+    def out_cols(self) -> int:
+        """Forces kept per instance (12 x the output steps, 12 N by default)."""
+        steps = getattr(self, "_out_steps", 0)
+        return 12 * (steps if 0 < steps < self.horizon else self.horizon)
+
+    def set_output_steps(self, steps: int) -> None:
+        """Keep the forces of the first ``steps`` horizon steps only (0: every step);
+        ``cmpc_batch_set_output_steps``: the forces' stride becomes 12 x steps."""
+        _check(self.lib.cmpc_batch_set_output_steps(self._h, int(steps)), "set_output_steps")
+        self._out_steps = int(steps)
+
+    @property
     def record_words(self) -> int:
         return record_words(self.params.horizon)
 
@@ -247,7 +261,7 @@ class BatchSolver:
             raise CmpcError(f"batch {batch} > max_batch {self.max_batch}")
         if hasattr(records, "shape"):
             assert records.shape[-1] == self.record_words, "record stride mismatch"
-            assert forces.numel() >= batch * 12 * self.horizon and status.numel() >= batch
+            assert forces.numel() >= batch * self.out_cols and status.numel() >= batch
         _check(self.lib.cmpc_batch_solve(self._h, _ptr(records), int(batch), _ptr(forces),
                                          _ptr(status), _ptr(iters)), "cmpc_batch_solve")
 
@@ -256,7 +270,7 @@ class BatchSolver:
         records = np.ascontiguousarray(records, np.float32)
         B = records.shape[0]
         assert records.shape[1] == self.record_words
-        forces = np.zeros((B, 12 * self.horizon), np.float32)
+        forces = np.zeros((B, self.out_cols), np.float32)
         status = np.zeros(B, np.uint8)
         iters = np.zeros(B, np.int32)
         _check(self.lib.cmpc_batch_solve_host(self._h, records.ctypes.data_as(_fp), B,

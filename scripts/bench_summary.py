@@ -17,5 +17,7 @@ for k, v in (d.get("other_configs") or {}).items():
 sm = d.get("scaling_model")
 if sm:
     print("scaling", [(r["gpus"], r.get("speedup"), r.get("t_solve_ms_measured")) for r in sm["rows"]])
+    print("scaling step-0 output", [(r["gpus"], r.get("step0_speedup"), r.get("step0_t_solve_ms_measured"))
+                                    for r in sm["rows"]])
 if d.get("cpu_baseline"):
     print("cpu", d["cpu_baseline"].get("value"))

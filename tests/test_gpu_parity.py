@@ -486,3 +486,44 @@ def test_batch_size_invariance(cm, solver_mod, N):
             np.testing.assert_array_equal(f1[0], f_all[i], err_msg=f"instance {i}, n = {n[i]}")
     finally:
         s1.close()
+
+
+@pytest.mark.parametrize("N,steps", [(10, 1), (10, 4), (20, 1)])
+def test_output_steps_keep_leading_forces_bitwise(cm, solver_mod, N, steps):
+    """cmpc_batch_set_output_steps(steps): the forces of the leading steps only (stride 12 x steps)
+    are bit for bit the leading columns of the full output, in every size class (random contact
+    tables: class 1, the tail class and the wide classes), through the device and the host entry
+    points and through a world-1 RootPipeline."""
+    import torch
+    par = importlib.import_module("quad-periodic-mpc_amd.parallel")
+    prm = cm.make_params(N)
+    B = 4096
+    recs = cm.make_instances(B, N, seed=9500 + N, random_contact_frac=1.0)
+    f_full, st_full, it_full = gpu_solve(solver_mod, prm, recs)
+    oc = 12 * steps
+    s = solver_mod.BatchSolver(prm, max_batch=B)
+    try:
+        s.set_output_steps(steps)
+        assert s.out_cols == oc
+        f_h, st_h, _ = s.solve_host(recs)
+        assert f_h.shape == (B, oc)
+        np.testing.assert_array_equal(f_h, f_full[:, :oc])
+        np.testing.assert_array_equal(st_h, st_full)
+        rd = torch.from_numpy(recs).cuda()
+        fd = torch.full((B, oc), -1.0, dtype=torch.float32, device="cuda")
+        sd = torch.empty(B, dtype=torch.uint8, device="cuda")
+        s.solve(rd, fd, sd)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(fd.cpu().numpy(), f_full[:, :oc])
+        f1, st1, _ = s.solve_host(recs[:1])  # the single-instance fast path
+        np.testing.assert_array_equal(f1[0], f_full[0, :oc])
+    finally:
+        s.close()
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        pipe = par.RootPipeline(prm, B, chunks=2, device="cuda", out_steps=steps)
+        pipe.step(torch.from_numpy(recs).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(pipe.forces.cpu().numpy(), f_full[:, :oc])
+    pipe.close()
