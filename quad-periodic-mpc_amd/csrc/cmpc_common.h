@@ -120,9 +120,19 @@ __device__ __forceinline__ int tid_opq() {
 
 // lane id (0..63) from mbcnt, opaque to the optimiser: unlike threadIdx.x (v0 at entry, which
 // has to stay live, or be spilled, to be re-read later) it needs no register between uses
+#ifndef CMPC_LANE_ASM
+#define CMPC_LANE_ASM 1
+#endif
 __device__ __forceinline__ int lane_opq() {
+#if CMPC_LANE_ASM
+  // the mbcnt pair inside the asm: every call recomputes the lane id (two VALU ops) instead of
+  // sharing one CSE'd value that lives across the kernel (and was spilled and reloaded per call)
+  int x;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
+#else
   int x = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   asm volatile("" : "+v"(x));
+#endif
   return x;
 }
 
@@ -170,6 +180,19 @@ struct F4x2 {
 
 // An SGPR value the compiler cannot see through: keeps per-iteration scalar work of an unrolled
 // loop inside its iteration (otherwise LICM hoists dozens of SGPRs out of it -> spills).
+// a constant or kernel argument materialised at its use (volatile asm is never hoisted): keeps
+// loop-invariant code motion from holding it in a register across a loop nest
+__device__ __forceinline__ float vopq(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ float sopq(float x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+__device__ __forceinline__ float rfl(float x) {  // a wave-uniform float into an SGPR
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
 __device__ __forceinline__ int opaque(int x) {
   x = __builtin_amdgcn_readfirstlane(x);
   asm volatile("" : "+s"(x));
@@ -363,7 +386,8 @@ __device__ __forceinline__ void make_bdt(const float* __restrict__ rec, const Mo
 }
 
 // rpy of the record's quaternion as the reference's quat_to_rpy (SolverMPC.cpp:352-361), fp32
-__device__ __forceinline__ void quat_to_rpy(const float* __restrict__ rec, float* rpy) {
+template <typename RecPtr>  // const float* or a global-address-space pointer
+__device__ __forceinline__ void quat_to_rpy(RecPtr rec, float* rpy) {
   const float qw = rec[CMPC_REC_Q + 0], qx = rec[CMPC_REC_Q + 1], qy = rec[CMPC_REC_Q + 2],
               qz = rec[CMPC_REC_Q + 3];
   float as = -2.f * (qx * qz - qw * qy);

@@ -64,6 +64,12 @@
 #ifndef CMPC_DIAG_REF_SKIP  // diagnostic builds: skip refinement phases (bit 0..4 = A..E; wrong results)
 #define CMPC_DIAG_REF_SKIP 0
 #endif
+#ifndef CMPC_REF_BFA_MAX  // phases A / D branch-free over the feet / rows up to this width
+#define CMPC_REF_BFA_MAX 96
+#endif
+#ifndef CMPC_REF_BFD_MAX
+#define CMPC_REF_BFD_MAX 96
+#endif
 #ifndef CMPC_REFINE_MAX
 #define CMPC_REFINE_MAX 4
 #endif
@@ -76,6 +82,7 @@ namespace cmpc {
 namespace {
 
 constexpr int kNoneW = 0x7fffffff;
+typedef __attribute__((address_space(1))) float gfloat;
 
 template <int NV>
 struct WGeo {
@@ -293,7 +300,9 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
   const float* rec = reinterpret_cast<const float*>(&sh.P[0]);
   (void)rec_in;
 #else
-  const float* rec = rec_in;
+  // global address space: the opaque pointer would otherwise be generic (flat loads, which wait
+  // on the LDS counter too)
+  const gfloat* rec = (const gfloat*)(rec_in);
   asm volatile("" : "+s"(rec));
 #endif
   double* scr = reinterpret_cast<double*>(&sh.P[G::O_RINV]);
@@ -307,7 +316,7 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
       const int k = t / 3, a = t - 3 * (t / 3);
       const int a1 = (a == 2) ? 0 : a + 1, a2 = (a == 0) ? 2 : a - 1;
       double tc = 0.0, sc = 0.0;
-      if constexpr (NV <= 96) {
+      if constexpr (NV <= CMPC_REF_BFA_MAX) {
         // branch-free over the feet: the lever arms (one global round trip for all eight) and the
         // step's four stance bytes (one LDS word) first, so every x read's address is known up front
         // (per-lane stance branches had serialised a load round trip per foot)
@@ -376,7 +385,7 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
       const uint32_t flags = __float_as_uint(rec[CMPC_REC_FLAGS]);
       scr[18] = (double)rec[CMPC_REC_XDRAG];
       scr[19] = (flags & 1u) ? (double)rec[CMPC_REC_FEST3] : 0.0;  // Q_qp f (SolverMPC.cpp:808-811)
-      scr[20] = (double)(-9.8f);
+      scr[20] = (double)vopq(-9.8f);
     } else if (t == G::NT - 20) {
       float rpy[3];  // x0's rpy as the fp32 solve computes it (quat_to_rpy)
       quat_to_rpy(rec, rpy);
@@ -390,7 +399,7 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
   if (!(CMPC_DIAG_REF_SKIP & 2)) {
     const double* R = scr;
     const double* Ii = scr + 9;
-    const float* traj = rec + CMPC_REC_HDR;
+    const auto traj = rec + CMPC_REC_HDR;
     double dv[2] = {0.0, 0.0};
 #pragma unroll
     for (int it = 0; it < 2; it++) {
@@ -499,18 +508,22 @@ __device__ __forceinline__ void refine_residual(const float* __restrict__ rec_in
       const double* R = scr;
       const double* Ii = scr + 9;
       const double xd = scr[18];
-      if constexpr (NV <= 96) {
+      if constexpr (NV <= CMPC_REF_BFD_MAX) {
         // branch-free over i (one instruction stream per wave; per-row branches cost 1 % at N = 16,
         // r04_k16): i < 3 y_k,i = (I_w^-1 nu[6:9])_i; 3..5 nu[9 + i - 3] / m
+        // (scheduling fences between the terms: with every LDS load hoisted to the top, the 30-odd
+        // fp64 operands were the refining builds' register peak and spilled the J rows' neighbours)
         const int ic = (i < 3) ? i : 0, il = (i < 3) ? 0 : i - 3;
+        const double x3 = (i == 3) ? xd : 0.0;
+        const double e2 = (dt * mu[9 + il] + dth * (mu[3 + il] + x3 * mu[11]) + dt3 * x3 * mu[5]) * (1.0 / 12.0);
+        __builtin_amdgcn_sched_barrier(0);
         double e1 = 0.0;
 #pragma unroll
         for (int m = 0; m < 3; m++) {
           const double nu = dt * mu[6 + m] + dth * (R[3 * m] * mu[0] + R[3 * m + 1] * mu[1] + R[3 * m + 2] * mu[2]);
           e1 += Ii[3 * ic + m] * nu;
+          __builtin_amdgcn_sched_barrier(0);
         }
-        const double x3 = (i == 3) ? xd : 0.0;
-        const double e2 = (dt * mu[9 + il] + dth * (mu[3 + il] + x3 * mu[11]) + dt3 * x3 * mu[5]) * (1.0 / 12.0);
         ev = (i < 3) ? e1 : e2;
       } else {
         if (i < 3) {
@@ -540,10 +553,10 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
   using G = WGeo<NV>;
   constexpr int NH = G::NH;
   constexpr int NC = (NH + 63) / 64;
-  const float* rec = rec_in;
+  const gfloat* rec = (const gfloat*)(rec_in);
   asm volatile("" : "+s"(rec));
   double* scr = reinterpret_cast<double*>(&sh.P[G::O_RINV]);
-  refine_residual<NV>(rec, P, sh, wave);
+  refine_residual<NV>(rec_in, P, sh, wave);
   // ---- E: row r's gradient entry, u = J2' r, x -= J2 u
   float rr = 0.f;
   {
@@ -555,7 +568,7 @@ __device__ __forceinline__ void wide_refine(const float* __restrict__ rec_in, co
       const double* yk = scr + 24 + 12 * k;
       // (y x r_b)_a = y_a1 r_a2 - y_a2 r_a1
       const double cr = yk[a1] * (double)rec[CMPC_REC_R + 4 * a2 + b] - yk[a2] * (double)rec[CMPC_REC_R + 4 * a1 + b];
-      rr = (float)(2.0 * (cr + yk[3 + a]) + (double)P.alpha2 * (double)xv);
+      rr = (float)(2.0 * (cr + yk[3 + a]) + (double)sopq(P.alpha2) * (double)xv);
     }
   }
   float pa[NC], pb[NC];
@@ -1040,6 +1053,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         if (bid == kNoneW || best >= -tol) break;
         p = __builtin_amdgcn_readfirstlane(bid);
         cp = decode_cons(p, mui, sh.sub[p / 6]);
+        cp.bp = rfl(cp.bp);  // uniform: SGPRs, not loop-carried VGPRs
         up = 0.f;
       }
       if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
@@ -1201,7 +1215,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         for (int m = 0; m < RQ; m++)
           if (lane + 64 * m < q) u_a[m] = fmaf(-tt, r_a[m], u_a[m]);
       }
-      up += tt;
+      up = rfl(up + tt);
       if (!zero_step) xv = fmaf(tt, zv, xv);
       const bool add = !zero_step && t2 <= t1;
       const bool add_u = __builtin_amdgcn_readfirstlane((int)add) != 0;  // wave-uniform copy
@@ -1242,7 +1256,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         if (t < NV) {
           sh.vbuf()[lidx<NV>(t)] = 0.f;
           if (t < k || t > q - 2)
-            *reinterpret_cast<float2*>(&sh.cs()[2 * t + (t >= NH ? 4 : 0)]) = make_float2(1.f, 0.f);
+            *reinterpret_cast<float2*>(&sh.cs()[2 * t + (t >= NH ? 4 : 0)]) = make_float2(vopq(1.f), vopq(0.f));
         }
         if (wave == 0) {
           const int ak = rli_pos<RQ>(a_a, k);

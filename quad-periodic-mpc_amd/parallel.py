@@ -153,10 +153,11 @@ class ShardedSolver:
 
 
 # Smallest pipeline piece worth cutting. Every solve ends in a tail (its slowest instances, the
-# wide size classes) that a piece pays again; measured on one MI355X (scripts/occupancy_sweep.py):
-# 32768 instances in one solve 1.23 ms, in two pieces of 16384 2 x 0.83 ms; 65536 in one 1.8 ms.
-# The xGMI time a second piece could hide at 8 ranks (~0.25 ms per step) is less than the 0.4 ms
-# it costs, so pieces stay at >= 65536 instances.
+# wide size classes) that a piece pays again; measured on one MI355X (round 5, the bench's
+# scaling model, profiles/r05_w/bench.log): 32768 instances in one solve 0.91 ms, in two pieces of
+# 16384 1.31 ms; 65536 in one 1.47 ms, in two pieces 2.31 ms. The xGMI time a second piece could
+# hide at 8 ranks (~0.14 ms of scatter per step) is far less than the ~0.4 ms it costs, so pieces
+# stay at >= 65536 instances.
 MIN_PIECE = 65536
 MAX_CHUNKS = 4
 
@@ -164,7 +165,8 @@ MAX_CHUNKS = 4
 def auto_chunks(local_batch: int, world: int = 2, min_piece: int = MIN_PIECE,
                 max_chunks: int = MAX_CHUNKS) -> int:
     """Pieces per rank for the config-4 pipeline: one when there is no traffic to hide (world
-    1: 262144 records in one solve 6.59 ms, in four pieces 7.38 ms on one MI355X), else as many
+    1: 262144 records in one solve 5.4 ms on one MI355X, round 5; in four pieces ~12 % more,
+    round 4), else as many
     as keep every piece >= ``min_piece`` instances, at most ``max_chunks`` (262144 over 1 / 2 /
     4 / 8 ranks -> 1 / 2 / 1 / 1)."""
     if world <= 1:

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 profiling session: rocprofv3 kernel trace + stats of the bench workloads (configs 3, 2,
+# Profiling session: rocprofv3 kernel trace + stats of the bench workloads (configs 3, 2,
 # 5 and N = 16 trot), then the PMC counter passes (scripts/gpu_pmc_all.sh). Each GPU step has its
 # own time limit; the script stops at the first failure.
-# usage: scripts/gpu_profile_r04.sh <tag>
+# usage: scripts/gpu_profile.sh <tag>
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-TAG=${1:-r04_prof}
+TAG=${1:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp

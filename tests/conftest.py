@@ -16,6 +16,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
 
 
+# One line per parity check (tests/test_gpu_parity.py assert_parity / assert_failed_reference):
+# printed as a terminal-summary section, so a quiet run (-q, output captured) still shows how often
+# each case took the fp64-optimum branch and against which cap.
+PARITY_LEDGER = []
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    if PARITY_LEDGER:
+        terminalreporter.section("parity ledger: instances beyond 1e-4 of qpOASES per case")
+        for line in PARITY_LEDGER:
+            terminalreporter.write_line(line)
+
+
 @pytest.fixture(scope="session")
 def cm():
     return importlib.import_module("quad-periodic-mpc_amd")

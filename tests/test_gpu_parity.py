@@ -23,7 +23,7 @@ import importlib
 import numpy as np
 import pytest
 
-from conftest import GOLDEN_SETS, golden_params, load_golden, rel_force_err
+from conftest import GOLDEN_SETS, PARITY_LEDGER, golden_params, load_golden, rel_force_err
 
 pytestmark = pytest.mark.gpu
 
@@ -63,6 +63,8 @@ def assert_failed_reference(orc, recs, prm, f, st, st_ref, label=""):
         e = np.abs(f[i] - x64).max() / max(np.abs(x64).max(), 1.0)
         print(f"[parity] {label}: instance {i} (reference qpOASES ret {st_ref[i]}): ours vs the fp64 "
               f"optimum {e:.2e}, status {st[i]}")
+        PARITY_LEDGER.append(f"{label}: instance {i} where the reference's qpOASES fails (ret "
+                             f"{st_ref[i]}): ours within {e:.1e} of the fp64 optimum")
         assert st[i] == 0 and e <= FP64_BRANCH_TOL, (i, st[i], e)
     return len(idx)
 
@@ -93,15 +95,20 @@ def assert_parity(orc, recs, prm, f, q_ref, ok=None, label="", gait="trotting", 
             sc = max(np.abs(x64).max(), 1.0)
             e64s.append(np.abs(f[i] - x64).max() / sc)
             eref.append(np.abs(q_ok[b] - x64).max() / sc)
-        gait = recs[idx, 32 + 12 * prm.horizon:32 + 13 * prm.horizon].copy().view(np.uint8)
-        n_bad = 3 * (gait != 0).sum(1)
+        gbytes = recs[idx, 32 + 12 * prm.horizon:32 + 13 * prm.horizon].copy().view(np.uint8)
+        n_bad = 3 * (gbytes != 0).sum(1)
         print(msg + f" -> fp64-optimum branch: worst vs qpOASES {err[bad].max():.2e}, ours vs the "
               f"fp64 optimum <= {max(e64s):.2e}, the reference's {min(eref):.2e}..{max(eref):.2e}; "
               f"reduced sizes n {sorted(set(n_bad.tolist()))}, ours vs fp64 per instance "
               f"{[f'{e:.1e}' for e in e64s[:8]]}")
+        PARITY_LEDGER.append(f"{label} N={prm.horizon} {gait}: {len(bad)} of {len(err)} beyond 1e-4 "
+                             f"(cap {100 * cap:.1f} %, allowed {allowed:.1f}); ours vs fp64 <= "
+                             f"{max(e64s):.1e}, the reference's {min(eref):.1e}..{max(eref):.1e}")
         assert max(e64s) <= FP64_BRANCH_TOL, (err.max(), max(e64s))
         return
     print(msg)
+    PARITY_LEDGER.append(f"{label} N={prm.horizon} {gait}: 0 of {len(err)} beyond 1e-4 (max "
+                         f"{err.max():.1e})")
     assert len(bad) == 0, (err.max(), int(np.argmax(err)))
 
 
