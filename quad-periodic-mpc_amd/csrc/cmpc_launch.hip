@@ -147,7 +147,9 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   const int nsides = (tail && t8_pos == 2) ? 3 : 2;
   // the tail class's hand-offs, behind it on its stream: a one-workgroup persistent launch of the
   // 80-column class (it reads the final count once the tail class is done)
+  static const int handoff_env = diag_knob("CMPC_HANDOFF", 1);  // 0: no hand-off launch (timing A/B only)
   auto launch_handoff = [&](hipStream_t s) -> hipError_t {
+    if (!handoff_env) return hipSuccess;
     return launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[10], &cnt[11], &cnt[kDeq + 10],
                            kHandoffGrid, s);
   };
@@ -234,7 +236,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // critical path (config 3 timeline, profiles/r04_prof). CMPC_W120_SIDE=0/1 forces a side (A/B)
     static const int w120_env = diag_knob("CMPC_W120_SIDE", -1);
     const int w120_side = (w120_env >= 0) ? (w120_env & 1) : (6 * P.N <= 80 ? 1 : 0);
-    if (n_max > 96 && (e = launch_wide_w120(d_recs, P, d_forces, d_status, d_iters, list[8], &cnt[9],
+    static const int w120_skip = diag_knob("CMPC_SKIP_W120", 0);  // timing A/B only (n 97-120 unsolved)
+    if (n_max > 96 && !w120_skip && (e = launch_wide_w120(d_recs, P, d_forces, d_status, d_iters, list[8], &cnt[9],
                                             dq(8, 97, 120), grid_of[8], ctx.side[w120_side])) != hipSuccess)
       return e;
     if (n_max > 120 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
