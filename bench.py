@@ -245,6 +245,8 @@ def local_leg(args, cm, prm, config, N, B, steps, warmup, dev, rank, barrier, sy
     else:
         solver_mod = importlib.import_module("quad-periodic-mpc_amd.solver")
         solver = solver_mod.BatchSolver(prm, max_batch=B, stream=torch.cuda.current_stream(dev))
+        if args.no_refine:  # A/B only: the refinement off (cmpc_batch_set_refine(0)); noted in config
+            solver.set_refine(False)
 
         def step():
             solver.solve(recs, forces, status, iters)
@@ -505,6 +507,8 @@ def main():
     ap.add_argument("--random-contact-frac", type=float, default=0.25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip end-to-end / solve-only legs")
+    ap.add_argument("--no-refine", action="store_true",
+                    help="A/B only: the wide classes' fp64 refinement off (cmpc_batch_set_refine)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU ranks over gloo with a plumbing stand-in for the solve (no GPU)")
     args = ap.parse_args()
@@ -712,6 +716,8 @@ def main():
         "status_counts": status_counts,
         "forces_digest": digest(out_forces) if out_forces is not None else None,
     }
+    if getattr(args, "no_refine", False):
+        out["config"]["refine"] = "off (A/B run, cmpc_batch_set_refine(0): not the product setting)"
     if args.dry_run:
         out["dry_run"] = "gloo CPU ranks, plumbing stand-in for the solve (not a measurement)"
     out.update(extras)

@@ -218,6 +218,11 @@ CMPC_EXTERNC int cmpc_batch_solve(cmpc_batch* h, const float* d_records, int bat
  * (12N, the default). A caller that reads only get_solution(0..11) as ConvexMPCLocomotion.cpp:
  * 832-845 does can keep step 0 (48 B instead of 480 B per instance at N = 10). New API. */
 CMPC_EXTERNC int cmpc_batch_set_output_steps(cmpc_batch* h, int steps);
+/* The fp64 refinement of the converged working set in the wide size classes:
+ * 1 (default) from N = 11, 0 off (every horizon solved in fp32 only, as the reference's own fp32
+ * condensation: ~11 % faster at N = 16, but at N >= 16 a few all-stance instances then miss
+ * qpOASES by more than 1e-4). New API. */
+CMPC_EXTERNC int cmpc_batch_set_refine(cmpc_batch* h, int on);
 /* Same, host buffers in and out (H2D + solve + D2H on the handle's stream, synchronous). */
 CMPC_EXTERNC int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int batch,
                                        float* forces, uint8_t* status, int32_t* iters);

@@ -34,6 +34,7 @@ struct cmpc_batch {
   cmpc_params prm;
   cmpc::KParams kp;
   int out_steps = 0;             // cmpc_batch_set_output_steps (0: every step)
+  int refine = 1;                // cmpc_batch_set_refine (1: from N = 11, 0: off)
   int max_batch = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -189,7 +190,18 @@ extern "C" int cmpc_batch_set_params(cmpc_batch* h, const cmpc_params* prm) {
   h->prm = *prm;
   h->kp = make_kparams(*prm);
   if (h->out_steps > 0 && h->out_steps < prm->horizon) h->kp.out_cols = 12 * h->out_steps;
+  if (!h->refine) h->kp.refine = 0;
   return ensure_admm_slabs(h);
+}
+
+extern "C" int cmpc_batch_set_refine(cmpc_batch* h, int on) {
+  if (!h || on < 0 || on > 1) {
+    g_last_error = "cmpc_batch_set_refine: bad arguments";
+    return -1;
+  }
+  h->refine = on;
+  h->kp.refine = (on && h->prm.horizon >= CMPC_REFINE_FROM_N) ? 1 : 0;
+  return 0;
 }
 
 extern "C" int cmpc_batch_set_output_steps(cmpc_batch* h, int steps) {

@@ -86,7 +86,10 @@ bool one_per_entry(int lo, int hi, int N, int batch) {
   static const int form = diag_knob("CMPC_WIDE_FORM", 0);
   if (form == 1 || batch < 16384) return true;
   if (form == 2) return false;
-  const float mode = 6.f * (float)N, half = 3.f * sqrtf((float)N);
+  // CMPC_POP_F_HI (A/B): the populous half-width in standard deviations from N = 11 (default 1)
+  static const int pop_hi = diag_knob("CMPC_POP_F_HI", 100);
+  const float f = (N > 10) ? 0.01f * (float)pop_hi : 1.f;
+  const float mode = 6.f * (float)N, half = f * 3.f * sqrtf((float)N);
   return (float)hi >= mode - half && (float)lo <= mode + half;
 }
 

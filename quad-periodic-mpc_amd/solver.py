@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = (
     "update_problem_data_floats", "_Z13update_x_dragf", "f_ext", "simulation_time",
     "f_est", "f_est_smoothed", "f_est_static",
     "cmpc_record_words", "cmpc_batch_create", "cmpc_batch_set_params", "cmpc_batch_destroy",
-    "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_set_output_steps", "cmpc_batch_condense",
+    "cmpc_batch_solve", "cmpc_batch_solve_host", "cmpc_batch_set_output_steps", "cmpc_batch_set_refine",
+    "cmpc_batch_condense",
     "cmpc_batch_stream",
     "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_enable_timing_every", "cmpc_batch_read_timing", "cmpc_batch_estimate",
     "cmpc_batch_assemble", "cmpc_batch_rollout", "cmpc_batch_admm",
@@ -91,6 +92,8 @@ def load_library(path: str = LIB_PATH):
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.cmpc_batch_solve_host.argtypes = [ctypes.c_void_p, _fp, ctypes.c_int, _fp, _u8p, _ip]
     lib.cmpc_batch_set_output_steps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if hasattr(lib, "cmpc_batch_set_refine"):  # (older A/B variant libraries lack it)
+        lib.cmpc_batch_set_refine.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.cmpc_batch_condense.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p]
     lib.cmpc_batch_admm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -240,6 +243,11 @@ class BatchSolver:
         ``cmpc_batch_set_output_steps``: the forces' stride becomes 12 x steps."""
         _check(self.lib.cmpc_batch_set_output_steps(self._h, int(steps)), "set_output_steps")
         self._out_steps = int(steps)
+
+    def set_refine(self, on: bool) -> None:
+        """The wide classes' fp64 refinement (``cmpc_batch_set_refine``): on from N = 11 by
+        default; off solves every horizon in fp32 only."""
+        _check(self.lib.cmpc_batch_set_refine(self._h, 1 if on else 0), "set_refine")
 
     @property
     def record_words(self) -> int:

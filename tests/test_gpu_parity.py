@@ -245,6 +245,47 @@ def test_deployed_horizon_large_sample_live(cm, orc, solver_mod, gait):
     print(f"[parity] N=16 {gait} x{B}: {nf} instances where the reference's qpOASES fails")
 
 
+@pytest.mark.parametrize("gait", ["standing", "trotting"])
+def test_refine_switch_live(cm, orc, solver_mod, gait):
+    """cmpc_batch_set_refine (the refinement behind a parameter, with parity counts
+    for both settings). N = 16, 512 live instances: refinement on (the default) passes the gate;
+    off, the same kernels solve in fp32 only. Both settings' counts go to the parity ledger: how
+    many instances land beyond 1e-4 of qpOASES and how far ours are from the fp64 optimum there.
+    Switching back on reproduces the default bit for bit."""
+    if not orc.ref_available():
+        pytest.skip("oracle/_ref not present")
+    N, B = 16, 512
+    prm = cm.make_params(N)
+    recs = cm.make_instances(B, N, seed=93000 + N, random_contact_frac=0.0, gait=gait)
+    q, st_ref, _ = orc.ref_solve_batch(recs, prm, nthreads=16)
+    ok = st_ref == 0
+    s = solver_mod.BatchSolver(prm, max_batch=B)
+    try:
+        f_on, st_on, _ = s.solve_host(recs)
+        s.set_refine(False)
+        f_off, st_off, _ = s.solve_host(recs)
+        s.set_refine(True)
+        f_again, st_again, _ = s.solve_host(recs)
+    finally:
+        s.close()
+    assert (st_on[ok] == 0).all() and (st_off[ok] == 0).all()
+    assert np.array_equal(f_on, f_again) and np.array_equal(st_on, st_again)
+    assert not np.array_equal(f_on, f_off)  # the switch reaches the kernels
+    assert_parity(orc, recs, prm, f_on, q, ok, label=f"refine on {gait}", gait=gait)
+    err = rel_force_err(f_off[ok], q[ok])
+    bad = np.nonzero(err > tol_for(N))[0]
+    idx = np.nonzero(ok)[0]
+    e64 = []
+    for b in bad[:16]:  # (a sample: one fp64 solve per instance)
+        x64, ri = orc.fp64_solve(recs[idx[b]], prm)
+        if ri == 0:
+            e64.append(np.abs(f_off[idx[b]] - x64).max() / max(np.abs(x64).max(), 1.0))
+    line = (f"refine off N=16 {gait}: {len(bad)} of {ok.sum()} beyond 1e-4 (max {err.max():.1e})"
+            + (f"; ours vs fp64 on them {min(e64):.1e}..{max(e64):.1e}" if e64 else ""))
+    print("[parity] " + line)
+    PARITY_LEDGER.append(line)
+
+
 CLASS_EDGES = [0, 60, 64, 80, 96, 120, 128, 144, 192, 256]  # class 1 (60 / 64 builds), wide 80 .. 256
 
 
