@@ -379,11 +379,12 @@ def scaling_model(args, cm, dev, sync):
     """Config 4 at G = 1, 2, 4, 8 GPUs predicted from ONE GPU (a labelled model, not a
     measurement): every rank of a G-GPU run solves 262144 / G records cut into
     parallel.auto_chunks pieces, which a world-1 RootPipeline over that many records reproduces
-    exactly, so the per-rank solve time is measured here. Rank 0 scatters each piece's records to
-    G - 1 peers (one xGMI link each, concurrently) and gathers their forces back; only the first
-    scatter and the last gather are exposed, the rest overlaps the solve of the neighbouring
-    pieces unless it is longer than that solve. t_G = t_solve + t_first_scatter + t_last_gather
-    + max(0, comm of the inner pieces - t_solve); speedup = t_1 / t_G."""
+    exactly, so the per-rank solve times are measured here. Rank 0 sends each piece's records to
+    G - 1 peers (one xGMI link each, concurrently) and receives their forces back; only the first
+    send and the last receive are exposed, the rest overlaps the solve of the neighbouring pieces
+    unless it is longer than that solve. Root solves its own, larger share (parallel.rank_sizes)
+    without waiting for a transfer. t_G = max(t_root_solve, t_solve + t_first_scatter +
+    t_last_gather + max(0, comm of the inner pieces - t_solve)); speedup = t_1 / t_G."""
     import torch
     par = importlib.import_module("quad-periodic-mpc_amd.parallel")
     R = importlib.import_module("quad-periodic-mpc_amd.records")
@@ -409,13 +410,30 @@ def scaling_model(args, cm, dev, sync):
         pipe.close()
         return t, sizes
 
+    def model_t(t_peer_solve, t_root_solve, pieces, out_bytes, bw):
+        """The peers' path (first scatter, solve, last gather, exposed inner transfers) against
+        root's own solve, which waits for no transfer (parallel.RootPipeline)."""
+        sc = [p * rec_b / (bw * 1e9) for p in pieces]   # per-peer bytes of a piece / link
+        ga = [p * out_bytes / (bw * 1e9) for p in pieces]
+        inner = sum(sc[1:]) + sum(ga[:-1])
+        t_peer = t_peer_solve + sc[0] + ga[-1] + max(0.0, inner - t_peer_solve)
+        return max(t_peer, t_root_solve)
+
     for G in (1, 2, 4, 8):
-        local = G_total // G
-        # the pieces a G-rank run cuts each rank's shard into (world 1 itself solves in one piece)
-        t_solve, pieces = timed_pieces(local, par.auto_chunks(local, G))
+        # the rows of root and of a peer in a G-rank run (root keeps root_share_auto times a
+        # peer's rows, parallel.rank_sizes), cut into the pieces that run cuts them into
+        share = par.root_share_auto(R.record_words(N), 12 * N) if G > 1 else 1.0
+        sizes_r = par.rank_sizes(G_total, G, 0, share)
+        local, root_local = sizes_r[-1], sizes_r[0]
+        chunks = par.auto_chunks(max(sizes_r), G)
+        t_solve, pieces = timed_pieces(local, chunks)
         row = {"gpus": G, "per_rank_instances": local, "pieces": len(pieces),
                "piece_instances": pieces[0], "t_solve_ms_measured": round(t_solve * 1e3, 4)}
-        if G > 1:   # the other piece count, for comparison (pieces alternate over two handles)
+        if G > 1:
+            t_root, _ = timed_pieces(root_local, chunks)
+            row.update(root_instances=root_local, root_share=round(share, 3),
+                       t_root_solve_ms_measured=round(t_root * 1e3, 4))
+            # the other piece count, for comparison (pieces alternate over two handles)
             alt = 1 if len(pieces) > 1 else 2
             t_alt, _ = timed_pieces(local, alt)
             row["t_solve_ms_measured_with_%d_pieces" % alt] = round(t_alt * 1e3, 4)
@@ -424,26 +442,26 @@ def scaling_model(args, cm, dev, sync):
             row.update(t_model_ms=round(t_solve * 1e3, 4), speedup=1.0)
         else:
             for bw, key in ((XGMI_LINK_GBS, ""), (50.0, "_at_50GBs")):
-                sc = [p * rec_b / (bw * 1e9) for p in pieces]   # per-peer bytes of a piece / link
-                ga = [p * out_b / (bw * 1e9) for p in pieces]
-                inner = sum(sc[1:]) + sum(ga[:-1])
-                t = t_solve + sc[0] + ga[-1] + max(0.0, inner - t_solve)
+                t = model_t(t_solve, t_root, pieces, out_b, bw)
                 row["t_model_ms" + key] = round(t * 1e3, 4)
                 row["speedup" + key] = round(t1 / t, 3)
-            row["xgmi_mb_root_sends"] = round((G - 1) * local * rec_b / 1e6, 2)
-            row["xgmi_mb_root_receives"] = round((G - 1) * local * out_b / 1e6, 2)
+            row["xgmi_mb_root_sends"] = round((G_total - root_local) * rec_b / 1e6, 2)
+            row["xgmi_mb_root_receives"] = round((G_total - root_local) * out_b / 1e6, 2)
         # the same with the step-0 forces only (cmpc_batch_set_output_steps(1): what a caller of
         # get_solution(0..11) reads, ConvexMPCLocomotion.cpp:832-845): 48 B gathered per instance
-        t0s, _ = timed_pieces(local, par.auto_chunks(local, G), out_steps=1)
+        # (root's share follows the smaller transfer)
+        share0 = par.root_share_auto(R.record_words(N), 12) if G > 1 else 1.0
+        sizes0 = par.rank_sizes(G_total, G, 0, share0)
+        chunks0 = par.auto_chunks(max(sizes0), G)
+        t0s, pieces0 = timed_pieces(sizes0[-1], chunks0, out_steps=1)
         row["step0_t_solve_ms_measured"] = round(t0s * 1e3, 4)
         if G == 1:
             t1s = t0s
             row["step0_speedup"] = 1.0
         else:
-            sc = [p * rec_b / (XGMI_LINK_GBS * 1e9) for p in pieces]
-            ga = [p * 48 / (XGMI_LINK_GBS * 1e9) for p in pieces]
-            inner = sum(sc[1:]) + sum(ga[:-1])
-            t = t0s + sc[0] + ga[-1] + max(0.0, inner - t0s)
+            t0r, _ = timed_pieces(sizes0[0], chunks0, out_steps=1)
+            row.update(step0_root_instances=sizes0[0], step0_t_root_solve_ms_measured=round(t0r * 1e3, 4))
+            t = model_t(t0s, t0r, pieces0, 48, XGMI_LINK_GBS)
             row["step0_t_model_ms"] = round(t * 1e3, 4)
             row["step0_speedup"] = round(t1s / t, 3)
         rows.append(row)

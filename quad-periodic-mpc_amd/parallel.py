@@ -174,15 +174,43 @@ def auto_chunks(local_batch: int, world: int = 2, min_piece: int = MIN_PIECE,
     return max(1, min(max_chunks, local_batch // max(1, min_piece)))
 
 
-def _chunk_plan(batch: int, world: int, chunks: int):
-    """Per rank r and chunk c: rows [a_rc, b_rc) of the global batch (contiguous rank shards,
-    each split into ``chunks`` contiguous pieces) and S_c = the largest piece c over ranks (the
-    collective size; shorter pieces are padded)."""
-    plan = []
+# Root's share of the batch (RootPipeline): root solves its own rows where they lie, while every
+# other rank's rows first cross one xGMI link and their forces cross back. Balancing the ranks'
+# finishing times gives root 1 + (bytes moved per instance) / ROOT_EQUIV_BYTES times a peer's
+# rows: ROOT_EQUIV_BYTES is what one link (153 GB/s per direction) carries in the marginal solve
+# time of one instance at N = 10 (17.3 ns: 32768 vs 65536 instances in 0.91 vs 1.47 ms on one
+# MI355X, round 5, profiles/r05_w/bench.log). N = 10 with every step's forces: 1.43; step 0 only:
+# 1.27.
+ROOT_EQUIV_BYTES = 2650.0
+
+
+def root_share_auto(record_words: int, cols: int) -> float:
+    return 1.0 + 4.0 * (record_words + cols) / ROOT_EQUIV_BYTES
+
+
+def rank_sizes(batch: int, world: int, src: int = 0, root_share: float = 1.0) -> list[int]:
+    """Rows per rank: root ``src`` about ``root_share`` times a peer's, the peers within one of
+    each other (root_share 1: :func:`shard_sizes`)."""
+    if world <= 1 or root_share == 1.0:
+        return shard_sizes(batch, world)
+    peer = int(batch // (world - 1 + root_share))
+    root = batch - peer * (world - 1)
+    sizes = [peer] * world
+    sizes[src] = root
+    return sizes
+
+
+def _chunk_plan(batch: int, world: int, chunks: int, src: int = 0, root_share: float = 1.0):
+    """Per rank r and chunk c: rows [a_rc, b_rc) of the global batch (contiguous rank blocks of
+    :func:`rank_sizes`, each split into ``chunks`` contiguous pieces), and S_c = the largest
+    piece c over ranks (the solver handles' capacity)."""
+    sizes_r = rank_sizes(batch, world, src, root_share)
+    plan, a = [], 0
     for r in range(world):
-        a, b = shard_bounds(batch, world, r)
+        b = a + sizes_r[r]
         plan.append([(a + lo, a + hi) for lo, hi in
                      (shard_bounds(b - a, chunks, c) for c in range(chunks))])
+        a = b
     sizes = [max(plan[r][c][1] - plan[r][c][0] for r in range(world)) for c in range(chunks)]
     return plan, sizes
 
@@ -192,12 +220,17 @@ class RootPipeline:
     one :meth:`step` scatters them over the ranks (RCCL over xGMI under the ``nccl`` backend),
     solves every rank's contiguous shard on its own GPU and gathers the forces back to root.
 
+    The transfers are point-to-point (``batch_isend_irecv``: root sends each peer its rows and
+    receives its forces straight into :attr:`forces`, no staging or padding). Root solves its own
+    rows where they lie, without waiting for any transfer, so it takes ``root_share`` times a
+    peer's rows (default :func:`root_share_auto`: the ranks then finish together).
+
     The shard of every rank is cut into ``chunks`` pieces (default :func:`auto_chunks`) and the
-    three stages are software-pipelined: the collectives run on the process group's
+    three stages are software-pipelined: the transfers run on the process group's
     communication stream, the solve on the caller's current stream, so piece c+1 is in flight
-    over xGMI while piece c is being solved and piece c-1 is being gathered. Issue order per step (communication stream):
-    scatter 0, scatter 1, gather 0, scatter 2, gather 1, ... — a gather never delays the next
-    piece's scatter.
+    over xGMI while piece c is being solved and piece c-1 is being gathered. Issue order per step
+    (communication stream): scatter 0, scatter 1, gather 0, scatter 2, gather 1, ... — a gather
+    never delays the next piece's scatter.
 
     ``solve_fn(records, forces, status)`` solves rows in place (device tensors of this rank).
     The default solves the pieces on ``lanes`` (two) :class:`BatchSolver` handles, each on its
@@ -212,7 +245,8 @@ class RootPipeline:
 
     def __init__(self, params, global_batch: int, chunks: Optional[int] = None, *, group=None,
                  device=None, src: int = 0, solve_fn=None, record_words: Optional[int] = None,
-                 lanes: Optional[int] = None, out_steps: int = 0):
+                 lanes: Optional[int] = None, out_steps: int = 0,
+                 root_share: Optional[float] = None):
         from .records import record_words as _rw
         self.params = params
         self.N = params.horizon
@@ -221,45 +255,33 @@ class RootPipeline:
         self.group = group
         self.src = src
         self.world, self.rank = _group_info(group)
-        if chunks is None:   # adaptive: pieces of >= MIN_PIECE instances (auto_chunks)
-            chunks = auto_chunks(max(shard_sizes(self.batch, self.world)), self.world)
-        self.chunks = max(1, min(int(chunks), max(1, self.batch // max(1, self.world))))
-        self.plan, self.sizes = _chunk_plan(self.batch, self.world, self.chunks)
-        self.start, self.stop = shard_bounds(self.batch, self.world, self.rank)
-        self.local_batch = self.stop - self.start
-        self.device = device
-        dev = device
         # forces kept per instance: every step (12 N) or, with out_steps, the leading steps only
         # (cmpc_batch_set_output_steps: a caller of get_solution(0..11) gathers 48 B, not 480 B)
         self.out_steps = int(out_steps) if 0 < int(out_steps) < self.N else 0
         cols = 12 * (self.out_steps or self.N)
         self.cols = cols
+        if root_share is None:
+            root_share = root_share_auto(self.words, cols) if self.world > 1 else 1.0
+        self.root_share = float(root_share)
+        if chunks is None:   # adaptive: pieces of >= MIN_PIECE instances (auto_chunks)
+            chunks = auto_chunks(max(shard_sizes(self.batch, self.world)), self.world)
+        self.chunks = max(1, min(int(chunks), max(1, self.batch // max(1, self.world))))
+        self.plan, self.sizes = _chunk_plan(self.batch, self.world, self.chunks, src, self.root_share)
+        self.start, self.stop = self.plan[self.rank][0][0], self.plan[self.rank][-1][1]
+        self.local_batch = self.stop - self.start
+        self.device = device
+        dev = device
         # this rank's rows: records in, forces / status out (chunk c = rows of plan[rank][c])
         self._last_root = None
-        # at world 1 the records are solved where they lie (no local copy)
-        self.local_recs = torch.zeros((self.local_batch if self.world > 1 else 0, self.words),
-                                      dtype=torch.float32, device=dev)
-        self.local_forces = torch.zeros((self.local_batch, cols), dtype=torch.float32, device=dev)
-        self.local_status = torch.zeros(self.local_batch, dtype=torch.uint8, device=dev)
+        # root (and world 1) solves its rows where they lie, into its rows of `forces`: no copies
+        is_root = self.rank == src
         self.forces = (torch.zeros((self.batch, cols), dtype=torch.float32, device=dev)
-                       if self.rank == src else None)
-        # padded staging only where a piece is shorter than its collective size
-        self._recv = {}
-        self._send = {}
-        self._root_send = {}
-        self._root_recv = {}
-        for c in range(self.chunks):
-            S = self.sizes[c]
-            a, b = self._local(c)
-            if b - a < S:
-                self._recv[c] = torch.zeros((S, self.words), dtype=torch.float32, device=dev)
-                self._send[c] = torch.zeros((S, cols), dtype=torch.float32, device=dev)
-            if self.rank == src:
-                for r in range(self.world):
-                    ra, rb = self.plan[r][c]
-                    if rb - ra < S:
-                        self._root_send[(r, c)] = torch.zeros((S, self.words), dtype=torch.float32, device=dev)
-                        self._root_recv[(r, c)] = torch.zeros((S, cols), dtype=torch.float32, device=dev)
+                       if is_root else None)
+        self.local_recs = torch.zeros((0 if is_root else self.local_batch, self.words),
+                                      dtype=torch.float32, device=dev)
+        self.local_forces = (self.forces[self.start:self.stop] if is_root else
+                             torch.zeros((self.local_batch, cols), dtype=torch.float32, device=dev))
+        self.local_status = torch.zeros(self.local_batch, dtype=torch.uint8, device=dev)
         self._solve_fn = solve_fn
         self._solver = None
         self._solvers = []
@@ -311,6 +333,8 @@ class RootPipeline:
         a, b = self._local(c)
         if b <= a:
             return
+        if recs is None and self.rank == self.src:  # root: its rows of the records it holds
+            recs = self._last_root[self.start + a:self.start + b]
         recs = self.local_recs[a:b] if recs is None else recs
         forces = self.local_forces[a:b] if forces is None else forces
         status = self.local_status[a:b] if status is None else status
@@ -330,47 +354,41 @@ class RootPipeline:
         for st in self._streams:
             cur.wait_stream(st)
 
+    def _p2p(self, ops):
+        return dist.batch_isend_irecv(ops) if ops else []
+
     def _scatter(self, records_root, c):
-        S = self.sizes[c]
-        a, b = self._local(c)
-        out = self._recv.get(c, self.local_recs[a:a + S])
-        lst = None
+        """Piece c's records to the peers (root: one send per peer; a peer: one receive)."""
         if self.rank == self.src:
-            lst = []
-            for r in range(self.world):
-                ra, rb = self.plan[r][c]
-                if (r, c) in self._root_send:
-                    buf = self._root_send[(r, c)]
-                    buf[:rb - ra].copy_(records_root[ra:rb])
-                    lst.append(buf)
-                else:
-                    lst.append(records_root[ra:rb])
-        return dist.scatter(out, lst, src=self.src, group=self.group, async_op=True)
+            ops = [dist.P2POp(dist.isend, records_root[ra:rb], self._peer(r), self.group)
+                   for r, (ra, rb) in ((r, self.plan[r][c]) for r in range(self.world))
+                   if r != self.src and rb > ra]
+        else:
+            a, b = self._local(c)
+            ops = ([dist.P2POp(dist.irecv, self.local_recs[a:b], self._peer(self.src), self.group)]
+                   if b > a else [])
+        return self._p2p(ops)
 
     def _gather(self, c):
-        S = self.sizes[c]
-        a, b = self._local(c)
-        if c in self._send:
-            self._send[c][:b - a].copy_(self.local_forces[a:b])
-            send = self._send[c]
+        """Piece c's forces back to root, straight into its rows of `forces`."""
+        if self.rank == self.src:
+            ops = [dist.P2POp(dist.irecv, self.forces[ra:rb], self._peer(r), self.group)
+                   for r, (ra, rb) in ((r, self.plan[r][c]) for r in range(self.world))
+                   if r != self.src and rb > ra]
         else:
-            send = self.local_forces[a:a + S]
-        lst = None
-        if self.rank == self.src:
-            lst = []
-            for r in range(self.world):
-                ra, rb = self.plan[r][c]
-                lst.append(self._root_recv[(r, c)] if (r, c) in self._root_recv
-                           else self.forces[ra:rb])
-        return dist.gather(send, lst, dst=self.src, group=self.group, async_op=True)
+            a, b = self._local(c)
+            ops = ([dist.P2POp(dist.isend, self.local_forces[a:b], self._peer(self.src), self.group)]
+                   if b > a else [])
+        return self._p2p(ops)
 
-    def _finish_gather(self, c, work):
-        work.wait()
-        if self.rank == self.src:
-            for r in range(self.world):
-                if (r, c) in self._root_recv:
-                    ra, rb = self.plan[r][c]
-                    self.forces[ra:rb].copy_(self._root_recv[(r, c)][:rb - ra])
+    def _peer(self, r):
+        """Global rank of group rank r (P2POp takes global ranks)."""
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    @staticmethod
+    def _wait(works):
+        for w in works:
+            w.wait()
 
     def step(self, records_root: Optional[torch.Tensor]) -> None:
         """One pass: scatter -> solve -> gather, pipelined over the chunks. On root the forces of
@@ -397,17 +415,18 @@ class RootPipeline:
         for c in range(C):
             if c + 1 < C:
                 sc[c + 1] = self._scatter(records_root, c + 1)
-            # on piece c's lane: wait for its scatter, solve, then its gather (the collective
-            # waits for this stream, i.e. for piece c's solve, not for the other lane's)
+            # on piece c's lane: a peer waits for its records, solves, then sends its forces (the
+            # send waits for this stream, i.e. for piece c's solve, not for the other lane's);
+            # root solves its own rows at once and posts the receives of the peers' forces
             with _on(self._lane(c)[1]):
-                sc[c].wait()
-                if c in self._recv:
-                    a, b = self._local(c)
-                    self.local_recs[a:b].copy_(self._recv[c][:b - a])
+                if self.rank != self.src:
+                    self._wait(sc[c])
                 self._solve_piece(c)
                 ga[c] = self._gather(c)
         for c in range(C):
-            self._finish_gather(c, ga[c])
+            self._wait(ga[c])
+            if self.rank == self.src:
+                self._wait(sc[c])
         if cur is not None:
             self._join(cur)
 

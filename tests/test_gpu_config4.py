@@ -112,7 +112,7 @@ def _worker(rank, world, port, out_path, q):
         solver_mod.load_library()
         prm = cm.make_params(N)
         recs = torch.from_numpy(cm.make_instances(BATCH, N, seed=SEED)) if rank == 0 else None
-        solver = solver_mod.BatchSolver(prm, max_batch=BATCH // (4 * world) + 1)
+        solver = solver_mod.BatchSolver(prm, max_batch=BATCH // 4 + 1)  # root keeps the larger share
 
         def gpu_piece(r, f, st):   # CPU rows in, CPU rows out, solved on cuda:0
             rd = r.cuda()

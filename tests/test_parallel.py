@@ -85,3 +85,21 @@ def test_shard_bounds_cover_batch():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         par.shard_bounds(10, 2, 2)
+
+
+def test_rank_sizes_root_share():
+    """RootPipeline's plan: root keeps about root_share times a peer's rows (it solves them where
+    they lie), the peers split the rest evenly, the blocks cover the batch in rank order."""
+    par = importlib.import_module("quad-periodic-mpc_amd.parallel")
+    share = par.root_share_auto(164, 120)   # N = 10 records, every step's forces
+    assert 1.4 < share < 1.46
+    for batch, world in ((262144, 8), (262144, 2), (10007, 3), (5, 4)):
+        sizes = par.rank_sizes(batch, world, 0, share)
+        assert sum(sizes) == batch and len(sizes) == world
+        assert max(sizes[1:]) - min(sizes[1:]) <= 1
+        if batch >= 1000:
+            assert abs(sizes[0] / sizes[1] - share) < 0.01
+        plan, _ = par._chunk_plan(batch, world, 2, 0, share)
+        rows = [r for rank in plan for piece in rank for r in range(*piece)]
+        assert rows == list(range(batch))
+    assert par.rank_sizes(100, 3, 0, 1.0) == par.shard_sizes(100, 3)
