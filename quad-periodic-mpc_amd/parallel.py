@@ -409,24 +409,35 @@ class RootPipeline:
             if cur is not None:
                 self._join(cur)
             return
+        if self.rank == self.src:
+            # root: every send, then every receive of the peers' forces, posted at once from the
+            # caller's stream (in the order each peer issues its receives and sends), so no peer
+            # waits for root's own solve; then root solves its rows where they lie
+            sc = [self._scatter(records_root, c) for c in range(C)]
+            ga = [self._gather(c) for c in range(C)]
+            for c in range(C):
+                with _on(self._lane(c)[1]):
+                    self._solve_piece(c)
+            for c in range(C):
+                self._wait(ga[c])
+                self._wait(sc[c])
+            if cur is not None:
+                self._join(cur)
+            return
         sc = [None] * C
         ga = [None] * C
         sc[0] = self._scatter(records_root, 0)
         for c in range(C):
             if c + 1 < C:
                 sc[c + 1] = self._scatter(records_root, c + 1)
-            # on piece c's lane: a peer waits for its records, solves, then sends its forces (the
-            # send waits for this stream, i.e. for piece c's solve, not for the other lane's);
-            # root solves its own rows at once and posts the receives of the peers' forces
+            # on piece c's lane: wait for its records, solve, then send its forces (the send waits
+            # for this stream, i.e. for piece c's solve, not for the other lane's)
             with _on(self._lane(c)[1]):
-                if self.rank != self.src:
-                    self._wait(sc[c])
+                self._wait(sc[c])
                 self._solve_piece(c)
                 ga[c] = self._gather(c)
         for c in range(C):
             self._wait(ga[c])
-            if self.rank == self.src:
-                self._wait(sc[c])
         if cur is not None:
             self._join(cur)
 
