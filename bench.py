@@ -690,12 +690,14 @@ def main():
     pct = int(args.random_contact_frac * 100)
     mix = f"A1 trot at random phase + {pct}% Bernoulli(0.5) contact tables"
     if config == 4:
+        peer = (B_total - B_local) // max(1, world - 1) if world > 1 else 0
         workload = (f"BASELINE config 4: {B_total} instances in total (N={N}, {mix}) on rank 0's "
-                    f"GPU; per step RCCL scatter over xGMI -> per-rank solve of its contiguous "
-                    f"shard ({B_local}) -> gather of the forces to rank 0, pipelined over "
-                    f"{pipe.chunks} pieces per rank")
+                    f"GPU; per step RCCL point-to-point sends over xGMI -> per-rank solve of its "
+                    f"contiguous shard (rank 0 {B_local}, solved where it lies"
+                    + (f"; each peer {peer}" if world > 1 else "") +
+                    f") -> the forces back to rank 0, pipelined over {pipe.chunks} pieces per rank")
         metric, scaling = METRIC, "strong"
-        par_s = f"dp{world} (contiguous instance shards; RCCL scatter/gather)"
+        par_s = f"dp{world} (contiguous instance shards; RCCL send/recv)"
     elif config == 5:
         workload = (f"BASELINE config 5: horizon N={N}, per step one batched periodic-disturbance "
                     f"estimator step (LogData residual, Gaussian band-pass, DFT sine fit; "
