@@ -147,7 +147,7 @@ struct SharedC1 {
     float BdtT[12][16];    // prep + condensation: Bdt transposed
     float ibuf[NL];        // Cholesky + J: 1 / sqrt(d_k) of pivot k
     struct {               // active set
-      float bufA[NL], bufB[NL];  // published J rows ia, iz (contiguous: bufA[NL + c] = bufB[c])
+      float bufA[NL], bufB[NL];  // published J rows ia (bufA) and iz (bufB + 16, running into cs)
       float cs[2 * NL];    // Givens (c, s) per column pair
     } gi;
   } u;
@@ -604,7 +604,9 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       // d = J' n+ : rows ia, iz of J through LDS (dword stores: wide stores would tie the row
       // registers into tuples)
       if (v == cp.ia || v == cp.iz) {  // both rows in one pass (two lanes per store)
-        const int boff = (v == cp.iz) ? NL : 0;  // bufB follows bufA
+        // lane iz's row 16 words past bufB's start (into cs, written only later in a drop trip):
+        // lanes ia and iz, neighbours in one half-wave, then store to different banks
+        const int boff = (v == cp.iz) ? NL + 16 : 0;
 #pragma unroll
         for (int c = 0; c < NV; c++) {
           sh.u.gi.bufA[boff + c] = slot[c];
@@ -612,7 +614,8 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         }
       }
       lsync();
-      const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.u.gi.bufA[v], cp.cb * sh.u.gi.bufB[v]) : cp.cb * sh.u.gi.bufB[v];
+      const float dv = (cp.ia != cp.iz) ? fmaf(cp.ca, sh.u.gi.bufA[v], cp.cb * sh.u.gi.bufB[16 + v])
+                                        : cp.cb * sh.u.gi.bufB[16 + v];
       const float dm = (v >= q && v < n) ? dv : 0.f;
       sh.vbuf()[v] = dm;
       lsync();
