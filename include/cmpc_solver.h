@@ -248,7 +248,9 @@ typedef struct cmpc_admm_settings {
  * doubles: 151 MB at N = 16, 236 MB at N = 20), allocated by the handle's FIRST cmpc_batch_admm
  * call and kept from then on (handles that never run ADMM never pay for them): make that first
  * call outside stream capture, and expect an allocation failure to surface there. d_forces
- * [batch * 12N] = the solution as float (0 for eliminated variables); d_status 0 = residual
+ * [batch * out_cols] = the solution as float (0 for eliminated variables), the leading steps the
+ * handle keeps (cmpc_batch_set_output_steps; 12N by default), so cmpc_batch_rollout reads ADMM
+ * forces with the same stride as the active-set solve's; d_status 0 = residual
  * below terminate, 1 = max_iter reached; d_iters (may be NULL). */
 CMPC_EXTERNC int cmpc_batch_admm(cmpc_batch* h, const float* d_records, const float* d_H,
                                  const float* d_g, int batch, const cmpc_admm_settings* s,

@@ -34,6 +34,8 @@ struct AdmmParams {
   float mu_inv;
   float f_max;
   int reduced;   // use_jcqp == 2: swing legs eliminated first (SolverMPC.cpp:859-950, 984-1053)
+  int out_cols;  // forces kept per instance (cmpc_batch_set_output_steps): the output stride, as
+                 // the active-set kernels and cmpc_batch_rollout use it
 };
 
 // fmat row k (0..4) of a 5x3 block, column a (SolverMPC.cpp:657-664)
@@ -272,9 +274,10 @@ __device__ bool admm_solve(const float* __restrict__ recs, const float* __restri
   }
   // q_soln[i] = jcqp.getSolution()[i] (SolverMPC.cpp:1057-1062)
   // q_soln: eliminated variables 0 (reduced), else reducedProblem / jcqp.getSolution()
-  for (int v = t; v < nf; v += kAdmmThreads) {
+  // (the leading ap.out_cols of them: 12 N unless the handle keeps fewer steps)
+  for (int v = t; v < ap.out_cols; v += kAdmmThreads) {
     const int c = sinv[v / 3];
-    forces[(size_t)inst * nf + v] = c < 0 ? 0.f : (float)sx[cur][3 * c + v % 3];
+    forces[(size_t)inst * ap.out_cols + v] = c < 0 ? 0.f : (float)sx[cur][3 * c + v % 3];
   }
   if (t == 0) {
     status[inst] = st;
@@ -319,7 +322,8 @@ hipError_t launch_admm(const float* d_recs, const float* d_H, const float* d_g, 
     return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
   AdmmParams ap{s.rho, s.sigma, s.alpha, s.terminate, s.max_iter, P.N, P.rec_words, P.mu_inv,
-                P.f_max, s.reduced ? 1 : 0};
+                P.f_max, s.reduced ? 1 : 0, P.out_cols};
+  if (ap.out_cols < 12 || ap.out_cols > 12 * P.N) return hipErrorInvalidValue;
   const bool small_possible = s.reduced || P.N <= kAdmmMaxN;
   const bool large_possible = 12 * P.N > kNV;
   if (large_possible && (!d_slabs || nslabs < 1)) return hipErrorInvalidValue;

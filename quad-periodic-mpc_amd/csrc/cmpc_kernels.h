@@ -118,8 +118,10 @@ hipError_t launch_tail(const float* d_recs, const KParams& P, float* d_forces, u
                        int32_t* d_iters, const int* in_list, const int* in_count, int* ovf_list,
                        int* ovf_count, int grid, hipStream_t stream);
 // the reduced sizes the tail class takes from the 80-column wide class: 64 < n <= 72 at N <= 10
-// (the horizons without the fp64 refinement of the wide classes)
-inline bool tail_class(const KParams& P, int n) { return !P.refine && n > 64 && n <= 72; }
+// (the horizons without the fp64 refinement of the wide classes; with the refinement switched
+// off, cmpc_batch_set_refine(0), the longer horizons keep the 80-column class, whose parity the
+// refine-off tests cover)
+inline bool tail_class(const KParams& P, int n) { return !P.refine && P.N <= 10 && n > 64 && n <= 72; }
 hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* d_one, hipStream_t stream,
                          bool allow_tail = true);

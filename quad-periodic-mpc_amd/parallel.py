@@ -215,6 +215,21 @@ def _chunk_plan(batch: int, world: int, chunks: int, src: int = 0, root_share: f
     return plan, sizes
 
 
+def issue_order(chunks: int) -> list[tuple[str, int]]:
+    """The order in which every rank posts RootPipeline's point-to-point batches for one step:
+    scatter 0, scatter 1, gather 0, scatter 2, gather 1, ..., gather C-1. Root and each peer post
+    the SAME sequence: under the nccl backend every ``batch_isend_irecv`` is queued in issue order
+    on one communication stream and a large send completes only once its receive is posted, so a
+    pair of ranks that posted these in different orders could each wait on the other's later op
+    (root posting every scatter before any gather deadlocks from three pieces)."""
+    order = [("scatter", 0)] if chunks > 0 else []
+    for c in range(chunks):
+        if c + 1 < chunks:
+            order.append(("scatter", c + 1))
+        order.append(("gather", c))
+    return order
+
+
 class RootPipeline:
     """BASELINE config 4 / SURVEY.md §8(e): the records of the whole batch live on root ``src``;
     one :meth:`step` scatters them over the ranks (RCCL over xGMI under the ``nccl`` backend),
@@ -229,8 +244,8 @@ class RootPipeline:
     three stages are software-pipelined: the transfers run on the process group's
     communication stream, the solve on the caller's current stream, so piece c+1 is in flight
     over xGMI while piece c is being solved and piece c-1 is being gathered. Issue order per step
-    (communication stream): scatter 0, scatter 1, gather 0, scatter 2, gather 1, ... — a gather
-    never delays the next piece's scatter.
+    (communication stream, :func:`issue_order`, the same on every rank): scatter 0, scatter 1,
+    gather 0, scatter 2, gather 1, ... — a gather never delays the next piece's scatter.
 
     ``solve_fn(records, forces, status)`` solves rows in place (device tensors of this rank).
     The default solves the pieces on ``lanes`` (two) :class:`BatchSolver` handles, each on its
@@ -273,6 +288,9 @@ class RootPipeline:
         dev = device
         # this rank's rows: records in, forces / status out (chunk c = rows of plan[rank][c])
         self._last_root = None
+        # (kind, piece, peers) of every point-to-point batch this rank posted, in order (tests
+        # check that root and each peer post theirs in the same order; bounded to the last step)
+        self.op_log: list[tuple[str, int, tuple[int, ...]]] = []
         # root (and world 1) solves its rows where they lie, into its rows of `forces`: no copies
         is_root = self.rank == src
         self.forces = (torch.zeros((self.batch, cols), dtype=torch.float32, device=dev)
@@ -354,7 +372,8 @@ class RootPipeline:
         for st in self._streams:
             cur.wait_stream(st)
 
-    def _p2p(self, ops):
+    def _p2p(self, kind, c, ops):
+        self.op_log.append((kind, c, tuple(op.peer for op in ops)))
         return dist.batch_isend_irecv(ops) if ops else []
 
     def _scatter(self, records_root, c):
@@ -367,7 +386,7 @@ class RootPipeline:
             a, b = self._local(c)
             ops = ([dist.P2POp(dist.irecv, self.local_recs[a:b], self._peer(self.src), self.group)]
                    if b > a else [])
-        return self._p2p(ops)
+        return self._p2p("scatter", c, ops)
 
     def _gather(self, c):
         """Piece c's forces back to root, straight into its rows of `forces`."""
@@ -379,7 +398,7 @@ class RootPipeline:
             a, b = self._local(c)
             ops = ([dist.P2POp(dist.isend, self.local_forces[a:b], self._peer(self.src), self.group)]
                    if b > a else [])
-        return self._p2p(ops)
+        return self._p2p("gather", c, ops)
 
     def _peer(self, r):
         """Global rank of group rank r (P2POp takes global ranks)."""
@@ -409,12 +428,18 @@ class RootPipeline:
             if cur is not None:
                 self._join(cur)
             return
+        self.op_log = []
         if self.rank == self.src:
-            # root: every send, then every receive of the peers' forces, posted at once from the
-            # caller's stream (in the order each peer issues its receives and sends), so no peer
-            # waits for root's own solve; then root solves its rows where they lie
-            sc = [self._scatter(records_root, c) for c in range(C)]
-            ga = [self._gather(c) for c in range(C)]
+            # root: every send and every receive of the peers' forces, posted at once from the
+            # caller's stream in issue_order (the order each peer posts its receives and sends:
+            # the nccl backend runs them in issue order), so no peer waits for root's own solve;
+            # then root solves its rows where they lie
+            sc, ga = [None] * C, [None] * C
+            for kind, c in issue_order(C):
+                if kind == "scatter":
+                    sc[c] = self._scatter(records_root, c)
+                else:
+                    ga[c] = self._gather(c)
             for c in range(C):
                 with _on(self._lane(c)[1]):
                     self._solve_piece(c)
@@ -426,10 +451,10 @@ class RootPipeline:
             return
         sc = [None] * C
         ga = [None] * C
-        sc[0] = self._scatter(records_root, 0)
-        for c in range(C):
-            if c + 1 < C:
-                sc[c + 1] = self._scatter(records_root, c + 1)
+        for kind, c in issue_order(C):
+            if kind == "scatter":
+                sc[c] = self._scatter(records_root, c)
+                continue
             # on piece c's lane: wait for its records, solve, then send its forces (the send waits
             # for this stream, i.e. for piece c's solve, not for the other lane's)
             with _on(self._lane(c)[1]):
@@ -443,6 +468,8 @@ class RootPipeline:
 
     def solve_only(self) -> None:
         """The same pieces solved with no collective (kernel-only rate of the shard)."""
+        if self.rank == self.src and self._last_root is None:
+            raise RuntimeError("RootPipeline.solve_only: root holds no records yet (call step first)")
         if self.world == 1:
             return self.step(self._last_root)
         cur = self._fork()

@@ -103,3 +103,68 @@ def test_rank_sizes_root_share():
         rows = [r for rank in plan for piece in rank for r in range(*piece)]
         assert rows == list(range(batch))
     assert par.rank_sizes(100, 3, 0, 1.0) == par.shard_sizes(100, 3)
+
+
+def test_issue_order_interleaves():
+    par = importlib.import_module("quad-periodic-mpc_amd.parallel")
+    assert par.issue_order(1) == [("scatter", 0), ("gather", 0)]
+    assert par.issue_order(3) == [("scatter", 0), ("scatter", 1), ("gather", 0), ("scatter", 2),
+                                  ("gather", 1), ("gather", 2)]
+
+
+def _pipe_worker(rank, world, port, batch, N, chunks, q):
+    try:
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        cm = importlib.import_module("quad-periodic-mpc_amd")
+        par = importlib.import_module("quad-periodic-mpc_amd.parallel")
+        prm = cm.make_params(N)
+        full = torch.from_numpy(cm.make_instances(batch, N, seed=7))
+
+        def fn(recs, forces, status):
+            forces.copy_(_fake_solve(recs[:, 32:], N))
+            status.zero_()
+
+        pipe = par.RootPipeline(prm, batch, chunks=chunks, solve_fn=fn)
+        if rank == 0:
+            with pytest.raises(RuntimeError):
+                pipe.solve_only()   # root holds no records before its first step
+        for _ in range(2):
+            pipe.step(full if rank == 0 else None)
+        if rank == 0:
+            assert torch.equal(pipe.forces, _fake_solve(full[:, 32:], N))
+        log = pipe.op_log
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, ("ok", log)))
+    except Exception as e:  # report to the parent instead of hanging it
+        q.put((rank, (repr(e), None)))
+
+
+@pytest.mark.parametrize("world,chunks", [(3, 3), (2, 4), (3, 4)])
+def test_root_pipeline_pairwise_op_order(world, chunks):
+    """under the nccl backend the point-to-point batches of a rank pair run in
+    issue order, so root and every peer must post theirs in the same sequence. Each rank's op
+    log, restricted to one peer, must read scatter/gather by piece in the same order on both
+    sides (world 2 and 3, 3 and 4 pieces), and the gathered forces must be complete."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    batch = 97
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, batch, 10, chunks, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v[0] == "ok" for v in results.values()), results
+    root_log = results[0][1]
+    for peer in range(1, world):
+        root_seq = [(k, c) for k, c, peers in root_log if peer in peers]
+        peer_seq = [(k, c) for k, c, peers in results[peer][1] if 0 in peers]
+        assert root_seq == peer_seq, (peer, root_seq, peer_seq)
+        assert len(peer_seq) == 2 * chunks
