@@ -20,8 +20,52 @@
 /* small dense helpers (row-major)                                                           */
 /* ---------------------------------------------------------------------------------------- */
 
+/* Summation order of the fp32 products of the condensation (sgemm_nn / sgemv below). Eigen's
+ * GEMM/GEMV kernels (SolverMPC.cpp:806-814) sum each dot product in an order set by its blocking
+ * and vector width, which the build's Eigen version and flags fix and which this container cannot
+ * reproduce (no Eigen). Three orders bracket it (oracle_set_sum_order; tests and
+ * scripts/branch_orders.py only):
+ *   0  sequential over k, the compiler's contraction (gcc -O3 -march=x86-64-v3: FMA) — default;
+ *   1  blocked k-outer: panels of 8 products summed by fused multiply-adds from zero, each panel's
+ *      sum then added to the running total (a register-blocked micro-kernel's order);
+ *   2  pairwise: every product rounded on its own, then summed by recursive halving. */
+static int g_sum_order = 0;
+void oracle_set_sum_order(int order) { g_sum_order = (order >= 0 && order <= 2) ? order : 0; }
+int oracle_sum_order(void) { return g_sum_order; }
+
+static float dot_pairwise(const float* prod, int n) {
+  if (n <= 2) return n <= 0 ? 0.f : (n == 1 ? prod[0] : prod[0] + prod[1]);
+  const int h = n / 2;
+  return dot_pairwise(prod, h) + dot_pairwise(prod + h, n - h);
+}
+
+/* sum_p a[p * sa] * b[p * sb] in order 1 or 2 (k <= 13 * CMPC_MAX_HORIZON) */
+static float dot_order(int k, const float* a, int sa, const float* b, int sb, int order) {
+  if (order == 1) {
+    float acc = 0.f;
+    for (int p0 = 0; p0 < k; p0 += 8) {
+      float panel = 0.f;
+      const int pe = p0 + 8 < k ? p0 + 8 : k;
+      for (int p = p0; p < pe; p++) panel = fmaf(a[(size_t)p * sa], b[(size_t)p * sb], panel);
+      acc += panel;
+    }
+    return acc;
+  }
+  float prod[13 * CMPC_MAX_HORIZON];
+  for (int p = 0; p < k; p++) {
+    volatile float t = a[(size_t)p * sa] * b[(size_t)p * sb];  /* rounded, never contracted */
+    prod[p] = t;
+  }
+  return dot_pairwise(prod, k);
+}
+
 /* C[m x n] = A[m x k] * B[k x n], fp32 accumulate, C zeroed first. */
 static void sgemm_nn(int m, int n, int k, const float* A, const float* B, float* C) {
+  if (g_sum_order != 0) {
+    for (int i = 0; i < m; i++)
+      for (int j = 0; j < n; j++) C[(size_t)i * n + j] = dot_order(k, A + (size_t)i * k, 1, B + j, n, g_sum_order);
+    return;
+  }
   memset(C, 0, sizeof(float) * (size_t)m * n);
   for (int i = 0; i < m; i++) {
     float* c = C + (size_t)i * n;
@@ -48,6 +92,10 @@ static void sgemm_tn(int m, int n, int k, float alpha, const float* A, const flo
 
 /* y[m] = A[m x n] x[n] */
 static void sgemv(int m, int n, const float* A, const float* x, float* y) {
+  if (g_sum_order != 0) {
+    for (int i = 0; i < m; i++) y[i] = dot_order(n, A + (size_t)i * n, 1, x, 1, g_sum_order);
+    return;
+  }
   for (int i = 0; i < m; i++) {
     float s = 0.f;
     for (int j = 0; j < n; j++) s += A[(size_t)i * n + j] * x[j];

@@ -46,6 +46,12 @@ typedef struct oracle_red {
   char* con_elim;       /* [20N] */
 } oracle_red;
 
+/* Summation order of the condensation's fp32 dot products (process-wide; 0 = the default
+ * sequential order, 1 = blocked k-outer panels of 8, 2 = pairwise; cmpc_oracle.c). Only the
+ * summation-order spread of the fp64-branch evidence uses 1 and 2 (scripts/branch_orders.py). */
+void oracle_set_sum_order(int order);
+int oracle_sum_order(void);
+
 /* Condense one record (layout: include/cmpc_solver.h). qH/qg computed as the reference does. */
 int oracle_condense(const float* rec, const cmpc_params* prm, oracle_cond* out);
 

@@ -82,6 +82,7 @@ def ref():
         _ref.qpref_solve.argtypes = [ctypes.c_int, ctypes.c_int, _d, _d, _d, _d, _d,
                                      ctypes.c_int, _d, _i, _i]
         _ref.ref_solve_batch.argtypes = [_f, ctypes.c_int, ctypes.c_void_p, _d, _i, _i, ctypes.c_int]
+        _ref.oracle_set_sum_order.argtypes = [ctypes.c_int]
         _ref.oracle_condense.argtypes = [_f, ctypes.c_void_p, ctypes.POINTER(OracleCond)]
         _ref.ref_pipeline_c5_batch.argtypes = [_f, _f, _f, ctypes.c_int, ctypes.c_void_p,
                                                ctypes.c_float, _d, _i, ctypes.c_int]
@@ -217,17 +218,48 @@ def fp64_solve(rec: np.ndarray, prm):
     return out, ri
 
 
-def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1):
-    """Reference pipeline over a batch -> (q_soln [B, 12N] f64, status [B], nWSR [B])."""
+SUM_ORDERS = (0, 1, 2)   # cmpc_oracle.c oracle_set_sum_order: sequential, blocked k-outer, pairwise
+
+
+def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1, order: int = 0):
+    """Reference pipeline over a batch -> (q_soln [B, 12N] f64, status [B], nWSR [B]).
+
+    ``order`` selects the summation order of the restated condensation's fp32 dot products
+    (SUM_ORDERS; 0, the default, is the order every fixture was made with). Eigen's own order is
+    unknown here, so the fp64-branch evidence runs all three (scripts/branch_orders.py)."""
     B = records.shape[0]
     N = prm.horizon
     records = np.ascontiguousarray(records, np.float32)
     q = np.zeros((B, 12 * N))
     st = np.zeros(B, np.int32)
     nw = np.zeros(B, np.int32)
-    ref().ref_solve_batch(_fp(records), B, ctypes.byref(prm), q.ctypes.data_as(_d),
+    r = ref()
+    r.oracle_set_sum_order(int(order))
+    try:
+        r.ref_solve_batch(_fp(records), B, ctypes.byref(prm), q.ctypes.data_as(_d),
                           st.ctypes.data_as(_i), nw.ctypes.data_as(_i), int(nthreads))
+    finally:
+        r.oracle_set_sum_order(0)
     return q, st, nw
+
+
+def order_spread(rec: np.ndarray, prm, x64=None):
+    """The restated reference pipeline of one record under every summation order (SUM_ORDERS)
+    -> dict(q [3, 12N], st [3], e64 [3]: each order's distance from the fp64 optimum, spread: the
+    largest pairwise distance between the orders), distances norm-wise |.|_inf / max(|x64|_inf, 1)."""
+    rec = np.ascontiguousarray(np.asarray(rec, np.float32).reshape(1, -1))
+    if x64 is None:
+        x64, _ = fp64_solve(rec[0], prm)
+    sc = max(np.abs(x64).max(), 1.0)
+    qs, sts = [], []
+    for o in SUM_ORDERS:
+        q, st, _ = ref_solve_batch(rec, prm, nthreads=1, order=o)
+        qs.append(q[0])
+        sts.append(int(st[0]))
+    qs = np.array(qs)
+    e64 = np.abs(qs - x64[None]).max(axis=1) / sc
+    spread = max(np.abs(qs[a] - qs[b]).max() for a in range(3) for b in range(a + 1, 3)) / sc
+    return dict(q=qs, st=np.array(sts), e64=e64, spread=spread)
 
 
 def ref_pipeline_c5_batch(records: np.ndarray, logs: np.ndarray, est: np.ndarray, prm,
