@@ -81,9 +81,12 @@ def _threads():
 
 def cpu_baseline(prm, N: int, config5: bool = False):
     """The reference pipeline on the host cores (rank 0, N=1 only), bounded sample: the fp32
-    dense-S condensation restated from SolverMPC.cpp (oracle/cmpc_oracle.c) + the reference's
-    own qpOASES 3.2.0 compiled from its sources (oracle/_ref); at config 5 each instance also
-    runs the residual + estimator step first (SolverMPC.cpp:688-811, restated in C)."""
+    dense-S condensation restated from SolverMPC.cpp (oracle/cmpc_oracle.c) with its dense
+    products register-tiled the way Eigen's GEMM kernels run them (impl 1: bit for bit the naive
+    restatement's result, tests/test_oracle.py) + the reference's own qpOASES 3.2.0 compiled from
+    its sources (oracle/_ref); at config 5 each instance also runs the residual + estimator step
+    first (SolverMPC.cpp:688-811, restated in C). Throughput at the GPU's CPU share (16 threads)
+    and at every visible CPU; latency of one call on one core."""
     try:
         from oracle import oracle as orc
     except Exception:
@@ -92,48 +95,58 @@ def cpu_baseline(prm, N: int, config5: bool = False):
         return None
     cm = importlib.import_module("quad-periodic-mpc_amd")
     threads = _threads()
+    visible = _host_cpus()
     sample = 2048 if N >= 16 else 8192
     recs = cm.make_instances(sample, N)
+    R = importlib.import_module("quad-periodic-mpc_amd.records")
     if config5:
-        R = importlib.import_module("quad-periodic-mpc_amd.records")
         est, logs = _config5_state(cm, R, recs, sample)
-        orc.ref_pipeline_c5_batch(recs[:32].copy(), logs[:32], est[:32].copy(), prm, 10.4,
-                                  nthreads=threads)  # warm
-        t0 = time.perf_counter()
-        orc.ref_pipeline_c5_batch(recs, logs, est, prm, 10.4, nthreads=threads)
-        dt = time.perf_counter() - t0
-        what = ("residual + band-pass/DFT estimator step (SolverMPC.cpp:688-811, restated in C) "
-                "then ")
-    else:
-        orc.ref_solve_batch(recs[:64], prm, nthreads=threads)  # warm
-        t0 = time.perf_counter()
-        orc.ref_solve_batch(recs, prm, nthreads=threads)
-        dt = time.perf_counter() - t0
-        what = ""
+
+    def run(nthreads, k=sample, impl=1):
+        r = recs[:k].copy()
+        if config5:
+            e = est[:k].copy()
+            t0 = time.perf_counter()
+            orc.ref_pipeline_c5_batch(r, logs[:k], e, prm, 10.4, nthreads=nthreads, impl=impl)
+        else:
+            t0 = time.perf_counter()
+            orc.ref_solve_batch(r, prm, nthreads=nthreads, impl=impl)
+        return time.perf_counter() - t0
+
+    run(threads, 64)  # warm
+    dt = run(threads)
+    dt_all = run(visible) if visible > threads else None
     # per-call latency of the reference pipeline on one core (what one solveDenseMPC costs)
-    lat = recs[:256]
-    t1 = time.perf_counter()
-    if config5:
-        orc.ref_pipeline_c5_batch(lat.copy(), logs[:256], est[:256].copy(), prm, 10.4, nthreads=1)
-    else:
-        orc.ref_solve_batch(lat, prm, nthreads=1)
-    lat_us = (time.perf_counter() - t1) / lat.shape[0] * 1e6
-    return {"value": round(sample / dt, 1), "unit": "QP solves/s", "cores": threads,
-            "host_cpus_visible": _host_cpus(),
-            "cores_note": (f"capped at {CPU_THREAD_CAP} threads: the GPU box's CPU share per GPU "
-                           "(the visible count is the whole machine's)"),
-            "condensation_note": ("the condensation is the oracle's plain-C restatement of "
-                                  "SolverMPC.cpp's dense-S products (naive i-p-j loops, gcc -O3 "
-                                  "-march=x86-64-v3), not Eigen: slower per instance than the "
-                                  "reference's Eigen build (SURVEY §0.4 probe with an OpenBLAS "
-                                  "GEMM chain: ~175-205 us per instance); the QP stage is the "
-                                  "reference's own qpOASES"),
-            "kind": "reference", "latency_us_1core": round(lat_us, 1),
-            "sample": f"{sample} instances of the same synthetic workload (N={N}), per instance "
-                      f"{what}the solve_mpc equivalent: fp32 dense-S condensation "
-                      f"(SolverMPC.cpp:566-950 restated, oracle/cmpc_oracle.c) + reference "
-                      f"qpOASES 3.2.0 (setToMPC, nWSR=100) built from /root/reference; "
-                      f"{threads} std::threads; {dt:.2f} s wall"}
+    nlat = 256
+    lat_us = run(1, nlat) / nlat * 1e6
+    lat_naive_us = run(1, nlat, impl=0) / nlat * 1e6
+    what = ("residual + band-pass/DFT estimator step (SolverMPC.cpp:688-811, restated in C) then "
+            if config5 else "")
+    out = {"value": round(sample / dt, 1), "unit": "QP solves/s", "cores": threads,
+           "host_cpus_visible": visible,
+           "cores_note": (f"{threads} threads: the GPU box's CPU share per GPU; "
+                          f"value_all_visible_cpus: the same sample on {visible} threads"),
+           "value_all_visible_cpus": round(sample / dt_all, 1) if dt_all else None,
+           "latency_us_1core": round(lat_us, 1),
+           "latency_us_1core_naive_loops": round(lat_naive_us, 1),
+           "condensation_note": ("the dense-S products of SolverMPC.cpp:806-814 (B_qp^T S, (B_qp^T "
+                                 "S) B_qp, (2 B_qp^T) S and its product with the state error) as "
+                                 "dense register-tiled fp32 GEMMs (6 x 16 tiles, 8-wide FMA; "
+                                 "oracle/cmpc_oracle.c condense_blocked), the full dense work Eigen "
+                                 "does, summed in the same order as the naive loops (bit-identical "
+                                 "results); latency_us_1core_naive_loops times the naive loops"),
+           "kind": "reference",
+           "sample": f"{sample} instances of the same synthetic workload (N={N}), per instance "
+                     f"{what}the solve_mpc equivalent: fp32 dense-S condensation "
+                     f"(SolverMPC.cpp:566-950 restated, oracle/cmpc_oracle.c) + reference "
+                     f"qpOASES 3.2.0 (setToMPC, nWSR=100) built from /root/reference; "
+                     f"{threads} std::threads; {dt:.2f} s wall"}
+    try:
+        out["cpu_model"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                                if l.startswith("model name"))
+    except Exception:
+        pass
+    return out
 
 
 def _config5_state(cm, R, recs_np, B):

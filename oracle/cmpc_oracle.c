@@ -216,7 +216,111 @@ static inline uint8_t rec_gait(const float* rec, int N, int idx) {
 /* ---------------------------------------------------------------------------------------- */
 /* solve_mpc up to qH/qg (SolverMPC.cpp:566-814)                                             */
 /* ---------------------------------------------------------------------------------------- */
+/* ---- the blocked implementation of SolverMPC.cpp:806-814 (oracle_set_impl(1)) ----------------
+ * The same dense products as the naive loops (Eigen evaluates them densely: B_qp is a dense
+ * MatrixXf, S a dense 13N x 13N MatrixXf), register-tiled the way a GEMM micro-kernel is: a 6 x 16
+ * tile of C in vector registers, one B row panel and six A broadcasts per k. Every C element is
+ * still a sequential fused multiply-add over k from zero, the order of the naive loops compiled
+ * with contraction (gcc -O3 -march=x86-64-v3), so both give the same bits
+ * (tests/test_oracle.py::test_blocked_condensation_bitwise). qg's matrix-vector product runs over
+ * (2 S) B_qp, the transpose of (2 B_qp^T) S (each entry is the single product 2 S_jj B_ji), so the
+ * vector sweep runs along rows. CPU baseline only (bench.py cpu_baseline). */
+static int g_impl = 0;
+void oracle_set_impl(int impl) { g_impl = impl == 1 ? 1 : 0; }
+
+typedef float v8f __attribute__((vector_size(32)));
+#define PAD16(x) (((x) + 15) & ~15)
+#define PAD6(x) ((((x) + 5) / 6) * 6)
+
+static size_t blocked_ws_floats(int N) {
+  const size_t nx = 13u * N, nu = 12u * N, nxp = PAD16(nx), nup = PAD16(nu), mx6 = PAD6(nx);
+  return nu * nx + nx * nxp + nu * nxp + nx * nup + nu * nup + mx6 * nx + mx6 * nup + nup + 8 * 16;
+}
+
+#define LD8(p) (*(const v8f*)(p))   /* 32-B aligned: every buffer is 64-B aligned, ld % 16 == 0 */
+#define ST8(p, v) (*(v8f*)(p) = (v))
+
+/* C[M x Np] = A[M x K] (row stride lda) * B[K x Np] (ldb); M % 6 == 0, Np % 16 == 0 */
+static void gemm_tiled(int M, int Np, int K, const float* A, int lda, const float* B, int ldb, float* C,
+                       int ldc) {
+  for (int i0 = 0; i0 < M; i0 += 6) {
+    const float* a0 = A + (size_t)i0 * lda;
+    for (int j0 = 0; j0 < Np; j0 += 16) {
+      v8f c00 = {0}, c01 = {0}, c10 = {0}, c11 = {0}, c20 = {0}, c21 = {0};
+      v8f c30 = {0}, c31 = {0}, c40 = {0}, c41 = {0}, c50 = {0}, c51 = {0};
+      for (int k = 0; k < K; k++) {
+        const float* bk = B + (size_t)k * ldb + j0;
+        const v8f b0 = LD8(bk), b1 = LD8(bk + 8);
+        float a;
+        a = a0[k];           c00 += a * b0; c01 += a * b1;
+        a = a0[lda + k];     c10 += a * b0; c11 += a * b1;
+        a = a0[2 * lda + k]; c20 += a * b0; c21 += a * b1;
+        a = a0[3 * lda + k]; c30 += a * b0; c31 += a * b1;
+        a = a0[4 * lda + k]; c40 += a * b0; c41 += a * b1;
+        a = a0[5 * lda + k]; c50 += a * b0; c51 += a * b1;
+      }
+      float* c = C + (size_t)i0 * ldc + j0;
+      ST8(c, c00); ST8(c + 8, c01); c += ldc;
+      ST8(c, c10); ST8(c + 8, c11); c += ldc;
+      ST8(c, c20); ST8(c + 8, c21); c += ldc;
+      ST8(c, c30); ST8(c + 8, c31); c += ldc;
+      ST8(c, c40); ST8(c + 8, c41); c += ldc;
+      ST8(c, c50); ST8(c + 8, c51);
+    }
+  }
+}
+
+static float* align64(float* p) { return (float*)(((uintptr_t)p + 63) & ~(uintptr_t)63); }
+
+/* qH and qg as the naive code below computes them, through gemm_tiled */
+static void condense_blocked(int N, const float* Bqp, const float* w12, float alpha, const float* vec,
+                             float* qH, float* qg, float* ws) {
+  const int nx = 13 * N, nu = 12 * N, nxp = PAD16(nx), nup = PAD16(nu), mx6 = PAD6(nx);
+  float* Bt = align64(ws);
+  float* Sp = align64(Bt + (size_t)nu * nx);
+  float* T = align64(Sp + (size_t)nx * nxp);
+  float* Bp = align64(T + (size_t)nu * nxp);
+  float* Hp = align64(Bp + (size_t)nx * nup);
+  float* S2 = align64(Hp + (size_t)nu * nup);
+  float* T2t = align64(S2 + (size_t)mx6 * nx);
+  float* y = align64(T2t + (size_t)mx6 * nup);
+  /* the dense S (SolverMPC.cpp:624-630) and 2 S, B_qp^T and B_qp with padded rows */
+  memset(Sp, 0, sizeof(float) * (size_t)nx * nxp);
+  memset(S2, 0, sizeof(float) * (size_t)mx6 * nx);
+  for (int k = 0; k < N; k++)
+    for (int i = 0; i < 12; i++) {
+      const int d = 13 * k + i;
+      Sp[(size_t)d * nxp + d] = w12[i];
+      S2[(size_t)d * nx + d] = 2.f * w12[i];
+    }
+  for (int p = 0; p < nx; p++) {
+    for (int i = 0; i < nu; i++) Bt[(size_t)i * nx + p] = Bqp[(size_t)p * nu + i];
+    memcpy(Bp + (size_t)p * nup, Bqp + (size_t)p * nu, sizeof(float) * nu);
+    for (int i = nu; i < nup; i++) Bp[(size_t)p * nup + i] = 0.f;
+  }
+  gemm_tiled(nu, nxp, nx, Bt, nx, Sp, nxp, T, nxp);    /* B^T S */
+  gemm_tiled(nu, nup, nx, T, nxp, Bp, nup, Hp, nup);   /* (B^T S) B */
+  gemm_tiled(mx6, nup, nx, S2, nx, Bp, nup, T2t, nup); /* ((2 B^T) S)^T = (2 S) B */
+  for (int i = 0; i < nu; i++)
+    for (int j = 0; j < nu; j++) {
+      float h = Hp[(size_t)i * nup + j];
+      if (i == j) h += alpha;
+      qH[(size_t)i * nu + j] = 2.f * h;
+    }
+  for (int i0 = 0; i0 < nup; i0 += 8) {
+    v8f acc = {0};
+    for (int j = 0; j < nx; j++) acc += LD8(T2t + (size_t)j * nup + i0) * vec[j];
+    ST8(y + i0, acc);
+  }
+  memcpy(qg, y, sizeof(float) * nu);
+}
+
 size_t oracle_condense_ws_bytes(int N) {
+  const size_t nx = 13u * N, nu = 12u * N;
+  return sizeof(float) * (169u * (N + 1) + nx * 13 + nx * nu + nx * 6 + nx * nx + nu * nx + 2 * nx +
+                          blocked_ws_floats(N));
+}
+static size_t naive_ws_bytes(int N) {
   const size_t nx = 13u * N, nu = 12u * N;
   return sizeof(float) * (169u * (N + 1) + nx * 13 + nx * nu + nx * 6 + nx * nx + nu * nx + 2 * nx);
 }
@@ -277,7 +381,7 @@ int oracle_condense_ws(const float* rec, const cmpc_params* prm, oracle_cond* ou
   float* T = S + (size_t)nx * nx;
   float* vec = T + (size_t)nu * nx;
   float* tmp = vec + nx;
-  memset(ws, 0, oracle_condense_ws_bytes(N));
+  memset(ws, 0, naive_ws_bytes(N));
   float blk[13 * 12], qb[13 * 6];
   memset(pw, 0, sizeof(float) * 169);
   for (int i = 0; i < 13; i++) pw[i * 14] = 1.f;
@@ -300,8 +404,9 @@ int oracle_condense_ws(const float* rec, const cmpc_params* prm, oracle_cond* ou
     for (int i = 0; i < 12; i++) S[(size_t)(13 * k + i) * nx + 13 * k + i] = prm->weights[i];
   const float* traj = rec + CMPC_REC_TRAJ(N);
 
+  const int blocked = g_impl == 1 && out && out->qH && out->qg;
   /* qH = 2 (B^T S B + alpha I) (SolverMPC.cpp:806): (B^T S) B, as Eigen evaluates it. */
-  if (out && out->qH) {
+  if (out && out->qH && !blocked) {
     sgemm_tn(nu, nx, nx, 1.f, Bqp, S, T);
     sgemm_nn(nu, nu, nx, T, Bqp, out->qH);
     for (int i = 0; i < nu; i++)
@@ -325,8 +430,13 @@ int oracle_condense_ws(const float* rec, const cmpc_params* prm, oracle_cond* ou
         const float xd = (i < 12) ? traj[12 * k + i] : 0.f;
         vec[13 * k + i] = (vec[13 * k + i] + tmp[13 * k + i]) - xd;
       }
-    sgemm_tn(nu, nx, nx, 2.f, Bqp, S, T); /* (2 B^T) S, a second product as in the reference */
-    sgemv(nu, nx, T, vec, out->qg);
+    if (blocked) {
+      condense_blocked(N, Bqp, prm->weights, prm->alpha, vec, out->qH, out->qg,
+                       (float*)((char*)ws + naive_ws_bytes(N)));
+    } else {
+      sgemm_tn(nu, nx, nx, 2.f, Bqp, S, T); /* (2 B^T) S, a second product as in the reference */
+      sgemv(nu, nx, T, vec, out->qg);
+    }
   }
   if (out) {
     memcpy(out->x0, x0, sizeof(x0));

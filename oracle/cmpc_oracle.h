@@ -51,6 +51,9 @@ typedef struct oracle_red {
  * summation-order spread of the fp64-branch evidence uses 1 and 2 (scripts/branch_orders.py). */
 void oracle_set_sum_order(int order);
 int oracle_sum_order(void);
+/* Implementation of the dense qH / qg products: 0 the naive loops (default), 1 register-tiled
+ * GEMMs in the same summation order, bit for bit (the CPU baseline's; cmpc_oracle.c). */
+void oracle_set_impl(int impl);
 
 /* Condense one record (layout: include/cmpc_solver.h). qH/qg computed as the reference does. */
 int oracle_condense(const float* rec, const cmpc_params* prm, oracle_cond* out);

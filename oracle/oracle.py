@@ -83,6 +83,7 @@ def ref():
                                      ctypes.c_int, _d, _i, _i]
         _ref.ref_solve_batch.argtypes = [_f, ctypes.c_int, ctypes.c_void_p, _d, _i, _i, ctypes.c_int]
         _ref.oracle_set_sum_order.argtypes = [ctypes.c_int]
+        _ref.oracle_set_impl.argtypes = [ctypes.c_int]
         _ref.oracle_condense.argtypes = [_f, ctypes.c_void_p, ctypes.POINTER(OracleCond)]
         _ref.ref_pipeline_c5_batch.argtypes = [_f, _f, _f, ctypes.c_int, ctypes.c_void_p,
                                                ctypes.c_float, _d, _i, ctypes.c_int]
@@ -221,12 +222,14 @@ def fp64_solve(rec: np.ndarray, prm):
 SUM_ORDERS = (0, 1, 2)   # cmpc_oracle.c oracle_set_sum_order: sequential, blocked k-outer, pairwise
 
 
-def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1, order: int = 0):
+def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1, order: int = 0, impl: int = 0):
     """Reference pipeline over a batch -> (q_soln [B, 12N] f64, status [B], nWSR [B]).
 
     ``order`` selects the summation order of the restated condensation's fp32 dot products
     (SUM_ORDERS; 0, the default, is the order every fixture was made with). Eigen's own order is
-    unknown here, so the fp64-branch evidence runs all three (scripts/branch_orders.py)."""
+    unknown here, so the fp64-branch evidence runs all three (scripts/branch_orders.py).
+    ``impl`` 1 computes the dense qH / qg products with register-tiled GEMMs (same order, same bits:
+    the CPU baseline's implementation, cmpc_oracle.c condense_blocked)."""
     B = records.shape[0]
     N = prm.horizon
     records = np.ascontiguousarray(records, np.float32)
@@ -235,11 +238,13 @@ def ref_solve_batch(records: np.ndarray, prm, nthreads: int = 1, order: int = 0)
     nw = np.zeros(B, np.int32)
     r = ref()
     r.oracle_set_sum_order(int(order))
+    r.oracle_set_impl(int(impl))
     try:
         r.ref_solve_batch(_fp(records), B, ctypes.byref(prm), q.ctypes.data_as(_d),
                           st.ctypes.data_as(_i), nw.ctypes.data_as(_i), int(nthreads))
     finally:
         r.oracle_set_sum_order(0)
+        r.oracle_set_impl(0)
     return q, st, nw
 
 
@@ -263,7 +268,7 @@ def order_spread(rec: np.ndarray, prm, x64=None):
 
 
 def ref_pipeline_c5_batch(records: np.ndarray, logs: np.ndarray, est: np.ndarray, prm,
-                          sim_time: float, nthreads: int = 1):
+                          sim_time: float, nthreads: int = 1, impl: int = 0):
     """Config-5 reference pipeline, per instance: residual -> estimator step -> solve_mpc
     (records / est updated in place) -> (q_soln [B, 12N] f64, status [B])."""
     B = records.shape[0]
@@ -273,9 +278,14 @@ def ref_pipeline_c5_batch(records: np.ndarray, logs: np.ndarray, est: np.ndarray
     logs = np.ascontiguousarray(logs, np.float32)
     q = np.zeros((B, 12 * N))
     st = np.zeros(B, np.int32)
-    ref().ref_pipeline_c5_batch(_fp(records), _fp(logs), _fp(est), B, ctypes.byref(prm),
+    r = ref()
+    r.oracle_set_impl(int(impl))
+    try:
+        r.ref_pipeline_c5_batch(_fp(records), _fp(logs), _fp(est), B, ctypes.byref(prm),
                                 float(sim_time), q.ctypes.data_as(_d), st.ctypes.data_as(_i),
                                 int(nthreads))
+    finally:
+        r.oracle_set_impl(0)
     return q, st
 
 

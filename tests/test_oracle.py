@@ -199,3 +199,35 @@ def test_fp64_pipeline_close_to_reference(cm, orc):
             x64, ri = orc.fp64_solve(recs[i], prm)
             assert ri == 0 and st[i] == 0
             assert np.abs(q[i] - x64).max() / max(np.abs(x64).max(), 1.0) <= tol
+
+
+@pytest.mark.parametrize("N", [10, 16, 20])
+def test_blocked_condensation_bitwise(cm, orc, N):
+    """The CPU baseline's register-tiled dense products (oracle_set_impl(1), cmpc_oracle.c
+    condense_blocked) sum every dot product in the naive loops' order: the reference pipeline's
+    forces, status and nWSR are bit for bit those of the default implementation."""
+    if not orc.ref_available():
+        pytest.skip("oracle/_ref not present")
+    prm = cm.make_params(N)
+    recs = cm.make_instances(64, N, seed=4400 + N, random_contact_frac=0.5)
+    q0, s0, w0 = orc.ref_solve_batch(recs, prm, nthreads=4)
+    q1, s1, w1 = orc.ref_solve_batch(recs, prm, nthreads=4, impl=1)
+    np.testing.assert_array_equal(q0, q1)
+    np.testing.assert_array_equal(s0, s1)
+    np.testing.assert_array_equal(w0, w1)
+
+
+def test_summation_orders_bracket_the_default(cm, orc):
+    """The three summation orders of the restated condensation (oracle_set_sum_order) are three
+    valid fp32 evaluations of SolverMPC.cpp:806-814: at N = 10 (well conditioned) they agree with
+    each other within 1e-5 of the forces; order 0 is the golden fixtures' order (bitwise)."""
+    if not orc.ref_available():
+        pytest.skip("oracle/_ref not present")
+    g = load_golden("n10_mixed")
+    prm = golden_params(cm, g)
+    recs = g["records"][:16]
+    q = [orc.ref_solve_batch(recs, prm, nthreads=4, order=o)[0] for o in orc.SUM_ORDERS]
+    np.testing.assert_array_equal(q[0], g["q_ref"][:16])
+    for o in (1, 2):
+        assert rel_force_err(q[o], q[0]).max() <= 1e-5
+        assert not np.array_equal(q[o], q[0])   # the orders do round differently
