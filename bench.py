@@ -390,25 +390,31 @@ def make_roofline(launch_ms, ovf, units_per_launch, N, value, config):
 
 def scaling_model(args, cm, dev, sync):
     """Config 4 at G = 1, 2, 4, 8 GPUs predicted from ONE GPU (a labelled model, not a
-    measurement): every rank of a G-GPU run solves 262144 / G records cut into
+    measurement): every rank of a G-GPU run solves its block of the 262144 records cut into
     parallel.auto_chunks pieces, which a world-1 RootPipeline over that many records reproduces
-    exactly, so the per-rank solve times are measured here. Rank 0 sends each piece's records to
-    G - 1 peers (one xGMI link each, concurrently) and receives their forces back; only the first
-    send and the last receive are exposed, the rest overlaps the solve of the neighbouring pieces
-    unless it is longer than that solve. Root solves its own, larger share (parallel.rank_sizes)
-    without waiting for a transfer. t_G = max(t_root_solve, t_solve + t_first_scatter +
-    t_last_gather + max(0, comm of the inner pieces - t_solve)); speedup = t_1 / t_G."""
+    exactly (the compact records expanded on the GPU, then solved), so the per-rank times are
+    measured here. Rank 0 sends each piece's compact records (224 B at N = 10) to G - 1 peers (one
+    xGMI link each, concurrently) and receives their forces back; only the first send and the last
+    receive are exposed, the rest overlaps the solve of the neighbouring pieces unless it is longer
+    than that solve. Root solves its own, larger share (parallel.root_share_auto: 1 + bytes moved /
+    (pieces x 3213 B)) without waiting for a transfer. t_G = max(t_root, t_peer + t_first_scatter +
+    t_last_gather + max(0, comm of the inner pieces - t_peer)); speedup = t_1 / t_G."""
     import torch
     par = importlib.import_module("quad-periodic-mpc_amd.parallel")
     R = importlib.import_module("quad-periodic-mpc_amd.records")
     N, G_total = 10, 262144
     prm = cm.make_params(N)
-    rec_b = 4 * R.record_words(N)
+    words = R.compact_words(N)
+    rec_b = 4 * words
     out_b = 4 * 12 * N
-    recs_all = torch.from_numpy(cm.make_instances(G_total, N, random_contact_frac=args.random_contact_frac)).to(dev)
-    rows, t1 = [], None
+    full_np = cm.make_instances(G_total, N, random_contact_frac=args.random_contact_frac)
+    recs_all = torch.from_numpy(R.compact_records(full_np, N, prm.dt)).to(dev)
+    del full_np
+    rows = []
+
     def timed_pieces(local, chunks, out_steps=0):
-        pipe = par.RootPipeline(prm, local, chunks=chunks, device=dev, out_steps=out_steps)
+        pipe = par.RootPipeline(prm, local, chunks=chunks, device=dev, out_steps=out_steps,
+                                record_format="compact")
         recs = recs_all[:local]
         for _ in range(3):
             pipe.step(recs)
@@ -432,13 +438,15 @@ def scaling_model(args, cm, dev, sync):
         t_peer = t_peer_solve + sc[0] + ga[-1] + max(0.0, inner - t_peer_solve)
         return max(t_peer, t_root_solve)
 
+    def plan(G, cols):
+        chunks = par.auto_chunks(max(par.shard_sizes(G_total, G)), G)
+        share = par.root_share_auto(words, cols, chunks) if G > 1 else 1.0
+        return chunks, share, par.rank_sizes(G_total, G, 0, share)
+
+    t1 = t1s = None
     for G in (1, 2, 4, 8):
-        # the rows of root and of a peer in a G-rank run (root keeps root_share_auto times a
-        # peer's rows, parallel.rank_sizes), cut into the pieces that run cuts them into
-        share = par.root_share_auto(R.record_words(N), 12 * N) if G > 1 else 1.0
-        sizes_r = par.rank_sizes(G_total, G, 0, share)
+        chunks, share, sizes_r = plan(G, 12 * N)
         local, root_local = sizes_r[-1], sizes_r[0]
-        chunks = par.auto_chunks(max(sizes_r), G)
         t_solve, pieces = timed_pieces(local, chunks)
         row = {"gpus": G, "per_rank_instances": local, "pieces": len(pieces),
                "piece_instances": pieces[0], "t_solve_ms_measured": round(t_solve * 1e3, 4)}
@@ -446,10 +454,6 @@ def scaling_model(args, cm, dev, sync):
             t_root, _ = timed_pieces(root_local, chunks)
             row.update(root_instances=root_local, root_share=round(share, 3),
                        t_root_solve_ms_measured=round(t_root * 1e3, 4))
-            # the other piece count, for comparison (pieces alternate over two handles)
-            alt = 1 if len(pieces) > 1 else 2
-            t_alt, _ = timed_pieces(local, alt)
-            row["t_solve_ms_measured_with_%d_pieces" % alt] = round(t_alt * 1e3, 4)
         if G == 1:
             t1 = t_solve
             row.update(t_model_ms=round(t_solve * 1e3, 4), speedup=1.0)
@@ -462,10 +466,7 @@ def scaling_model(args, cm, dev, sync):
             row["xgmi_mb_root_receives"] = round((G_total - root_local) * out_b / 1e6, 2)
         # the same with the step-0 forces only (cmpc_batch_set_output_steps(1): what a caller of
         # get_solution(0..11) reads, ConvexMPCLocomotion.cpp:832-845): 48 B gathered per instance
-        # (root's share follows the smaller transfer)
-        share0 = par.root_share_auto(R.record_words(N), 12) if G > 1 else 1.0
-        sizes0 = par.rank_sizes(G_total, G, 0, share0)
-        chunks0 = par.auto_chunks(max(sizes0), G)
+        chunks0, share0, sizes0 = plan(G, 12)
         t0s, pieces0 = timed_pieces(sizes0[-1], chunks0, out_steps=1)
         row["step0_t_solve_ms_measured"] = round(t0s * 1e3, 4)
         if G == 1:
@@ -481,8 +482,9 @@ def scaling_model(args, cm, dev, sync):
     del recs_all
     return {"kind": "model (not a measurement): per-rank solve times measured on this GPU, "
                     f"xGMI at {XGMI_LINK_GBS:.0f} GB/s per link and direction (and a pessimistic "
-                    "50 GB/s), comm overlap per parallel.RootPipeline",
-            "global_batch": G_total, "horizon": N, "rows": rows}
+                    "50 GB/s), comm overlap per parallel.RootPipeline, compact records "
+                    f"({rec_b} B per instance) expanded on every rank",
+            "global_batch": G_total, "horizon": N, "record_bytes_sent": rec_b, "rows": rows}
 
 
 def other_configs(args, cm, dev, rank, barrier, sync, dist):
@@ -536,6 +538,9 @@ def main():
                     help="config-4 pipeline pieces per rank (default: parallel.auto_chunks)")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--random-contact-frac", type=float, default=0.25)
+    ap.add_argument("--record-format", choices=("compact", "full"), default="compact",
+                    help="config 4: the records root holds and sends (compact: trajAll's step-0 row, "
+                         "expanded on every rank by cmpc_batch_expand)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip end-to-end / solve-only legs")
     ap.add_argument("--no-refine", action="store_true",
@@ -589,12 +594,16 @@ def main():
     if config == 4:
         par = importlib.import_module("quad-periodic-mpc_amd.parallel")
         G = args.global_batch or 262144
+        R = importlib.import_module("quad-periodic-mpc_amd.records")
         pipe = par.RootPipeline(prm, G, chunks=args.chunks, device=dev,
-                                solve_fn=plumbing_solve(N) if args.dry_run else None)
+                                solve_fn=plumbing_solve(N) if args.dry_run else None,
+                                record_format=args.record_format)
         recs_root = None
         if rank == 0:
-            recs_root = torch.from_numpy(cm.make_instances(
-                G, N, random_contact_frac=args.random_contact_frac)).to(dev)
+            full_np = cm.make_instances(G, N, random_contact_frac=args.random_contact_frac)
+            if args.record_format == "compact":   # trajAll's step-0 row, expanded on every rank
+                full_np = R.compact_records(full_np, N, prm.dt)
+            recs_root = torch.from_numpy(full_np).to(dev)
         B_total, B_local = G, pipe.local_batch
 
         def step():
@@ -705,7 +714,8 @@ def main():
     if config == 4:
         peer = (B_total - B_local) // max(1, world - 1) if world > 1 else 0
         workload = (f"BASELINE config 4: {B_total} instances in total (N={N}, {mix}) on rank 0's "
-                    f"GPU; per step RCCL point-to-point sends over xGMI -> per-rank solve of its "
+                    f"GPU as {args.record_format} records ({4 * pipe.words} B each); per step RCCL "
+                    f"point-to-point sends over xGMI -> per-rank expansion + solve of its "
                     f"contiguous shard (rank 0 {B_local}, solved where it lies"
                     + (f"; each peer {peer}" if world > 1 else "") +
                     f") -> the forces back to rank 0, pipelined over {pipe.chunks} pieces per rank")

@@ -49,6 +49,15 @@
 #define CMPC_REC_GAIT(N)   (CMPC_REC_HDR + 12 * (N))
 #define CMPC_REC_WORDS(N)  ((CMPC_REC_HDR + 13 * (N) + 3) & ~3)
 
+/* Compact record (cmpc_batch_expand): what the caller computes trajAll from
+ * (ConvexMPCLocomotion.cpp:554-585) instead of trajAll itself — the header as above, trajAll's
+ * step-0 row (12 words: trajInitial with [2] = the measured yaw), the gait words, padding to a
+ * 16-byte multiple. 56 words (224 B) at N = 10 against 164 (656 B): what a root GPU sends each
+ * peer per instance in the config-4 sharding (parallel.RootPipeline record_format="compact"). */
+#define CMPC_CREC_TRAJ0    (CMPC_REC_HDR)
+#define CMPC_CREC_GAIT     (CMPC_REC_HDR + 12)
+#define CMPC_CREC_WORDS(N) ((CMPC_REC_HDR + 12 + (N) + 3) & ~3)
+
 #define CMPC_MAX_HORIZON  20  /* reference caps at 19 (SolverMPC.cpp:113-116); lifted to 20 for config 5;
                                  longer horizons are rejected (cmpc_batch_create / set_params -2) */
 
@@ -223,6 +232,13 @@ CMPC_EXTERNC int cmpc_batch_set_output_steps(cmpc_batch* h, int steps);
  * condensation: ~11 % faster at N = 16, but at N >= 16 a few all-stance instances then miss
  * qpOASES by more than 1e-4). New API. */
 CMPC_EXTERNC int cmpc_batch_set_refine(cmpc_batch* h, int on);
+/* Compact records (CMPC_CREC_*) -> solve records for the handle's horizon: trajAll[12 k + j] =
+ * the step-0 row, except j = 2, 3, 4 (yaw, x, y) = the previous step's + dtMPC x (yaw rate, v_x,
+ * v_y) of the step-0 row, in fp32 as updateMPCIfNeeded computes it (ConvexMPCLocomotion.cpp:
+ * 554-585, dtMPC = the handle's dt). Bit for bit the records a caller builds itself. d_compact
+ * [batch * CMPC_CREC_WORDS(N)], d_records [batch * cmpc_record_words(N)]. Asynchronous on the
+ * handle's stream. New API. */
+CMPC_EXTERNC int cmpc_batch_expand(cmpc_batch* h, const float* d_compact, float* d_records, int batch);
 /* Same, host buffers in and out (H2D + solve + D2H on the handle's stream, synchronous). */
 CMPC_EXTERNC int cmpc_batch_solve_host(cmpc_batch* h, const float* records, int batch,
                                        float* forces, uint8_t* status, int32_t* iters);

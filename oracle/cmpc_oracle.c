@@ -240,9 +240,64 @@ static size_t blocked_ws_floats(int N) {
 #define LD8(p) (*(const v8f*)(p))   /* 32-B aligned: every buffer is 64-B aligned, ld % 16 == 0 */
 #define ST8(p, v) (*(v8f*)(p) = (v))
 
+/* The same tile loop with 16-wide vectors where the host has AVX-512 (a 6 x 32 tile in twelve
+ * zmm accumulators, a 6 x 16 tile for the last 16 columns): each element is still one sequential
+ * fused multiply-add chain over k from zero, so both builds give the same bits. */
+typedef float v16f __attribute__((vector_size(64)));
+__attribute__((target("avx512f"))) static void gemm_tiled_512(int M, int Np, int K, const float* A, int lda,
+                                                              const float* B, int ldb, float* C, int ldc) {
+  for (int i0 = 0; i0 < M; i0 += 6) {
+    const float* a0 = A + (size_t)i0 * lda;
+    int j0 = 0;
+    for (; j0 + 32 <= Np; j0 += 32) {
+      v16f c00 = {0}, c01 = {0}, c10 = {0}, c11 = {0}, c20 = {0}, c21 = {0};
+      v16f c30 = {0}, c31 = {0}, c40 = {0}, c41 = {0}, c50 = {0}, c51 = {0};
+      for (int k = 0; k < K; k++) {
+        const float* bk = B + (size_t)k * ldb + j0;
+        const v16f b0 = *(const v16f*)bk, b1 = *(const v16f*)(bk + 16);
+        float a;
+        a = a0[k];           c00 += a * b0; c01 += a * b1;
+        a = a0[lda + k];     c10 += a * b0; c11 += a * b1;
+        a = a0[2 * lda + k]; c20 += a * b0; c21 += a * b1;
+        a = a0[3 * lda + k]; c30 += a * b0; c31 += a * b1;
+        a = a0[4 * lda + k]; c40 += a * b0; c41 += a * b1;
+        a = a0[5 * lda + k]; c50 += a * b0; c51 += a * b1;
+      }
+      float* c = C + (size_t)i0 * ldc + j0;
+      *(v16f*)c = c00; *(v16f*)(c + 16) = c01; c += ldc;
+      *(v16f*)c = c10; *(v16f*)(c + 16) = c11; c += ldc;
+      *(v16f*)c = c20; *(v16f*)(c + 16) = c21; c += ldc;
+      *(v16f*)c = c30; *(v16f*)(c + 16) = c31; c += ldc;
+      *(v16f*)c = c40; *(v16f*)(c + 16) = c41; c += ldc;
+      *(v16f*)c = c50; *(v16f*)(c + 16) = c51;
+    }
+    for (; j0 < Np; j0 += 16) {
+      v16f c0 = {0}, c1 = {0}, c2 = {0}, c3 = {0}, c4 = {0}, c5 = {0};
+      for (int k = 0; k < K; k++) {
+        const v16f b0 = *(const v16f*)(B + (size_t)k * ldb + j0);
+        c0 += a0[k] * b0;
+        c1 += a0[lda + k] * b0;
+        c2 += a0[2 * lda + k] * b0;
+        c3 += a0[3 * lda + k] * b0;
+        c4 += a0[4 * lda + k] * b0;
+        c5 += a0[5 * lda + k] * b0;
+      }
+      float* c = C + (size_t)i0 * ldc + j0;
+      *(v16f*)c = c0; *(v16f*)(c + ldc) = c1; *(v16f*)(c + 2 * ldc) = c2;
+      *(v16f*)(c + 3 * ldc) = c3; *(v16f*)(c + 4 * ldc) = c4; *(v16f*)(c + 5 * ldc) = c5;
+    }
+  }
+}
+
 /* C[M x Np] = A[M x K] (row stride lda) * B[K x Np] (ldb); M % 6 == 0, Np % 16 == 0 */
 static void gemm_tiled(int M, int Np, int K, const float* A, int lda, const float* B, int ldb, float* C,
                        int ldc) {
+  static int wide = -1;
+  if (wide < 0) wide = __builtin_cpu_supports("avx512f") ? 1 : 0;
+  if (wide) {
+    gemm_tiled_512(M, Np, K, A, lda, B, ldb, C, ldc);
+    return;
+  }
   for (int i0 = 0; i0 < M; i0 += 6) {
     const float* a0 = A + (size_t)i0 * lda;
     for (int j0 = 0; j0 < Np; j0 += 16) {

@@ -91,7 +91,33 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None,
     os.replace(tmp, lib)
     if out is None:
         build_tools(lib)
+        build_multi(lib)
     return lib
+
+
+MULTI_LIB = os.path.join(PKG, "libcmpc_multi.so")
+
+
+def build_multi(lib: str = LIB) -> str:
+    """libcmpc_multi.so (include/cmpc_multi.h): the config-4 sharding over RCCL as a C ABI, linked
+    against libcmpc_hip.so and librccl; plus its C++ test caller cmpc_multi_test."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    src = os.path.join(CSRC, "cmpc_multi.cpp")
+    hdrs = [os.path.join(ROOT, "include", h) for h in ("cmpc_multi.h", "cmpc_solver.h")]
+    if _stale(MULTI_LIB, [src, lib] + hdrs):
+        subprocess.run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-O2", "-std=c++17", "-fPIC",
+                        "-Wall", "-shared", "-o", MULTI_LIB + ".tmp", src, f"-L{PKG}", "-lcmpc_hip",
+                        "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{PKG}",
+                        "-Wl,-rpath,/opt/rocm/lib"], check=True)
+        os.replace(MULTI_LIB + ".tmp", MULTI_LIB)
+    exe = os.path.join(PKG, "cmpc_multi_test")
+    tsrc = os.path.join(CSRC, "tools", "cmpc_multi_test.cpp")
+    if _stale(exe, [tsrc, MULTI_LIB] + hdrs):
+        subprocess.run([hipcc, "-x", "hip", "--offload-arch=" + ARCH, "-O2", "-std=c++17", "-o", exe + ".tmp",
+                        tsrc, f"-L{PKG}", "-lcmpc_multi", "-lcmpc_hip", "-Wl,-rpath,$ORIGIN",
+                        f"-Wl,-rpath,{PKG}"], check=True)
+        os.replace(exe + ".tmp", exe)
+    return MULTI_LIB
 
 
 def build_tools(lib: str = LIB) -> str:

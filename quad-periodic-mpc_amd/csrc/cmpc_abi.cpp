@@ -342,6 +342,16 @@ extern "C" int cmpc_batch_assemble(cmpc_batch* h, float* d_loco, const cmpc_loco
   return 0;
 }
 
+extern "C" int cmpc_batch_expand(cmpc_batch* h, const float* d_compact, float* d_records, int batch) {
+  if (!h || batch < 0 || batch > h->max_batch || (batch && (!d_compact || !d_records))) {
+    g_last_error = "cmpc_batch_expand: bad arguments";
+    return -1;
+  }
+  hipError_t e = cmpc::launch_expand(d_compact, d_records, batch, h->kp.N, h->kp.rec_words, h->kp.dt, h->stream);
+  if (e != hipSuccess) return fail("launch_expand", e);
+  return 0;
+}
+
 extern "C" int cmpc_batch_rollout(cmpc_batch* h, float* d_loco, const float* d_records,
                                   const float* d_forces, const float* d_xi6, const uint8_t* d_due,
                                   int batch) {

@@ -406,6 +406,39 @@ __global__ __launch_bounds__(256) void cmpc_rollout_kernel(float* __restrict__ l
   s[CMPC_LOCO_Q + 3] = cr * cp * sy - sr * sp * cy;
 }
 
+// Compact records -> solve records (include/cmpc_solver.h CMPC_CREC_*): the header as is, trajAll
+// per updateMPCIfNeeded (ConvexMPCLocomotion.cpp:554-585) from its step-0 row — every step the
+// step-0 row, except trajAll[12 k + 2/3/4] = trajAll[12 (k-1) + 2/3/4] + dtMPC x (yaw rate, v_x,
+// v_y), fp32 product then fp32 sum as the caller computes them (this unit does not contract) —
+// and the gait words as is. One thread per output word, so the stores coalesce; the <= 20-step
+// recurrence is recomputed per word (the product is the same every step, so computing it once
+// rounds identically).
+__global__ __launch_bounds__(256) void cmpc_expand_kernel(const uint32_t* __restrict__ crec,
+                                                          uint32_t* __restrict__ recs, int batch, int N,
+                                                          int cw, int rw, float dt) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long long)batch * rw) return;
+  const int i = (int)(gid / rw), w = (int)(gid - (long long)i * rw);
+  const uint32_t* c = crec + (size_t)i * cw;
+  uint32_t v = 0u;
+  if (w < CMPC_REC_HDR) {
+    v = c[w];
+  } else if (w < CMPC_REC_GAIT(N)) {
+    const int k = (w - CMPC_REC_HDR) / 12, j = (w - CMPC_REC_HDR) % 12;
+    v = c[CMPC_CREC_TRAJ0 + j];
+    const int rate = (j == 2) ? 8 : (j == 3) ? 9 : (j == 4) ? 10 : -1;
+    if (rate >= 0 && k > 0) {
+      const float d = dt * __uint_as_float(c[CMPC_CREC_TRAJ0 + rate]);
+      float x = __uint_as_float(v);
+      for (int s = 1; s <= k; s++) x = x + d;
+      v = __float_as_uint(x);
+    }
+  } else if (w < CMPC_REC_GAIT(N) + N) {
+    v = c[CMPC_CREC_GAIT + (w - CMPC_REC_GAIT(N))];
+  }
+  recs[(size_t)i * rw + w] = v;
+}
+
 }  // namespace
 
 hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, uint8_t* d_due,
@@ -422,6 +455,16 @@ hipError_t launch_rollout(float* d_loco, const float* d_recs, const float* d_for
   if (batch <= 0) return hipSuccess;
   hipLaunchKernelGGL(cmpc_rollout_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, d_loco,
                      d_recs, d_forces, d_xi6, d_due, lp, dt, batch);
+  return hipGetLastError();
+}
+
+hipError_t launch_expand(const float* d_compact, float* d_recs, int batch, int N, int rec_words, float dt,
+                         hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  const long long words = (long long)batch * rec_words;
+  hipLaunchKernelGGL(cmpc_expand_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const uint32_t*>(d_compact), reinterpret_cast<uint32_t*>(d_recs), batch,
+                     N, CMPC_CREC_WORDS(N), rec_words, dt);
   return hipGetLastError();
 }
 

@@ -140,6 +140,9 @@ hipError_t launch_estimate(float* d_est, const float* d_logs, const float* d_fex
 // batched input assembly (cmpc_assemble.hip): one control tick per instance
 hipError_t launch_assemble(float* d_loco, const LocoParams& lp, float* d_recs, uint8_t* d_due,
                            int batch, hipStream_t stream);
+// compact records (CMPC_CREC_*) -> solve records, trajAll expanded per ConvexMPCLocomotion.cpp:554-585
+hipError_t launch_expand(const float* d_compact, float* d_recs, int batch, int N, int rec_words, float dt,
+                         hipStream_t stream);
 // single-rigid-body step of every due instance with its solved step-0 forces (cmpc_assemble.hip)
 hipError_t launch_rollout(float* d_loco, const float* d_recs, const float* d_forces,
                           const float* d_xi6, const uint8_t* d_due, const LocoParams& lp, float dt,

@@ -175,17 +175,18 @@ def auto_chunks(local_batch: int, world: int = 2, min_piece: int = MIN_PIECE,
 
 
 # Root's share of the batch (RootPipeline): root solves its own rows where they lie, while every
-# other rank's rows first cross one xGMI link and their forces cross back. Balancing the ranks'
-# finishing times gives root 1 + (bytes moved per instance) / ROOT_EQUIV_BYTES times a peer's
-# rows: ROOT_EQUIV_BYTES is what one link (153 GB/s per direction) carries in the marginal solve
-# time of one instance at N = 10 (17.3 ns: 32768 vs 65536 instances in 0.91 vs 1.47 ms on one
-# MI355X, round 5, profiles/r05_w/bench.log). N = 10 with every step's forces: 1.43; step 0 only:
-# 1.27.
-ROOT_EQUIV_BYTES = 2650.0
+# other rank's rows first cross one xGMI link and their forces cross back. With C pieces per rank
+# only the first piece's records and the last piece's forces are exposed on a peer (the rest
+# overlaps the solve), so balancing the ranks' finishing times gives root
+# 1 + (bytes moved per instance) / (C x ROOT_EQUIV_BYTES) times a peer's rows. ROOT_EQUIV_BYTES is
+# what one link (153 GB/s per direction) carries in the marginal solve time of one instance at
+# N = 10: 21 ns between 59192 and 84568 instances on one MI355X (the round-5 scaling model rows,
+# BENCH_r05.json). Round 5 used 2650 B and no 1 / C: 2 and 4 ranks were root-bound.
+ROOT_EQUIV_BYTES = 3213.0
 
 
-def root_share_auto(record_words: int, cols: int) -> float:
-    return 1.0 + 4.0 * (record_words + cols) / ROOT_EQUIV_BYTES
+def root_share_auto(record_words: int, cols: int, chunks: int = 1) -> float:
+    return 1.0 + 4.0 * (record_words + cols) / (max(1, chunks) * ROOT_EQUIV_BYTES)
 
 
 def rank_sizes(batch: int, world: int, src: int = 0, root_share: float = 1.0) -> list[int]:
@@ -261,11 +262,18 @@ class RootPipeline:
     def __init__(self, params, global_batch: int, chunks: Optional[int] = None, *, group=None,
                  device=None, src: int = 0, solve_fn=None, record_words: Optional[int] = None,
                  lanes: Optional[int] = None, out_steps: int = 0,
-                 root_share: Optional[float] = None):
-        from .records import record_words as _rw
+                 root_share: Optional[float] = None, record_format: str = "full"):
+        from .records import compact_words, record_words as _rw
         self.params = params
         self.N = params.horizon
-        self.words = record_words or _rw(self.N)
+        if record_format not in ("full", "compact"):
+            raise ValueError(f"record_format {record_format!r}: 'full' or 'compact'")
+        # "compact": root holds and sends compact records (include/cmpc_solver.h CMPC_CREC_*: trajAll's
+        # step-0 row instead of trajAll, 224 B instead of 656 B at N = 10); every rank expands its
+        # rows on its own GPU (cmpc_batch_expand) before solving them
+        self.compact = record_format == "compact"
+        self.full_words = _rw(self.N)
+        self.words = record_words or (compact_words(self.N) if self.compact else self.full_words)
         self.batch = int(global_batch)
         self.group = group
         self.src = src
@@ -275,12 +283,12 @@ class RootPipeline:
         self.out_steps = int(out_steps) if 0 < int(out_steps) < self.N else 0
         cols = 12 * (self.out_steps or self.N)
         self.cols = cols
-        if root_share is None:
-            root_share = root_share_auto(self.words, cols) if self.world > 1 else 1.0
-        self.root_share = float(root_share)
         if chunks is None:   # adaptive: pieces of >= MIN_PIECE instances (auto_chunks)
             chunks = auto_chunks(max(shard_sizes(self.batch, self.world)), self.world)
         self.chunks = max(1, min(int(chunks), max(1, self.batch // max(1, self.world))))
+        if root_share is None:
+            root_share = root_share_auto(self.words, cols, self.chunks) if self.world > 1 else 1.0
+        self.root_share = float(root_share)
         self.plan, self.sizes = _chunk_plan(self.batch, self.world, self.chunks, src, self.root_share)
         self.start, self.stop = self.plan[self.rank][0][0], self.plan[self.rank][-1][1]
         self.local_batch = self.stop - self.start
@@ -300,6 +308,9 @@ class RootPipeline:
         self.local_forces = (self.forces[self.start:self.stop] if is_root else
                              torch.zeros((self.local_batch, cols), dtype=torch.float32, device=dev))
         self.local_status = torch.zeros(self.local_batch, dtype=torch.uint8, device=dev)
+        # compact format: this rank's rows expanded into solve records before each piece's solve
+        self.full_recs = (torch.zeros((self.local_batch, self.full_words), dtype=torch.float32, device=dev)
+                          if self.compact else None)
         self._solve_fn = solve_fn
         self._solver = None
         self._solvers = []
@@ -356,6 +367,14 @@ class RootPipeline:
         recs = self.local_recs[a:b] if recs is None else recs
         forces = self.local_forces[a:b] if forces is None else forces
         status = self.local_status[a:b] if status is None else status
+        if self.compact:   # trajAll from its step-0 row, on this rank's GPU (cmpc_batch_expand)
+            full = self.full_recs[a:b]
+            if self._solve_fn is not None:
+                from .records import expand_records
+                full.copy_(torch.from_numpy(expand_records(recs.cpu().numpy(), self.N, self.params.dt)))
+            else:
+                self._lane(c)[0].expand(recs, full)
+            recs = full
         if self._solve_fn is not None:
             self._solve_fn(recs, forces, status)
         else:

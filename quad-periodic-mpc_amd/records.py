@@ -147,3 +147,52 @@ def pack_records(p, v, q, w, r, traj, gait, *, rpy=None, x_drag=None, f_est3=Non
 def unpack_gait(rec: np.ndarray, horizon: int) -> np.ndarray:
     off = gait_offset(horizon)
     return np.ascontiguousarray(rec[:, off:off + horizon]).view(np.uint8).reshape(rec.shape[0], 4 * horizon)
+
+
+# ---- compact records (include/cmpc_solver.h CMPC_CREC_*, cmpc_batch_expand) -------------------
+CREC_TRAJ0 = REC_HDR          # trajAll's step-0 row (12 words)
+CREC_GAIT = REC_HDR + 12      # the gait words
+
+
+def compact_words(horizon: int) -> int:
+    """CMPC_CREC_WORDS(N): header + trajAll's step-0 row + gait words, 16-B aligned."""
+    return (REC_HDR + 12 + horizon + 3) & ~3
+
+
+def expand_records(crec: np.ndarray, horizon: int, dt: float) -> np.ndarray:
+    """Host restatement of cmpc_batch_expand: trajAll per updateMPCIfNeeded
+    (ConvexMPCLocomotion.cpp:554-585) from its step-0 row, fp32 product then fp32 sum."""
+    N = horizon
+    crec = np.ascontiguousarray(crec, np.float32)
+    B = crec.shape[0]
+    out = np.zeros((B, record_words(N)), np.float32)
+    out[:, :REC_HDR] = crec[:, :REC_HDR]
+    row0 = crec[:, CREC_TRAJ0:CREC_TRAJ0 + 12]
+    traj = np.repeat(row0[:, None, :], N, axis=1)
+    d = np.float32(dt) * row0[:, [8, 9, 10]]          # yaw rate, v_x, v_y
+    for k in range(1, N):
+        traj[:, k, [2, 3, 4]] = traj[:, k - 1, [2, 3, 4]] + d
+    out[:, REC_HDR:REC_HDR + 12 * N] = traj.reshape(B, 12 * N)
+    out[:, gait_offset(N):gait_offset(N) + N] = crec[:, CREC_GAIT:CREC_GAIT + N]
+    return out
+
+
+def compact_records(recs: np.ndarray, horizon: int, dt: float) -> np.ndarray:
+    """Solve records -> compact records, for records whose trajAll has the form the controller
+    builds (ConvexMPCLocomotion.cpp:554-585; instances.make_instances and cmpc_batch_assemble
+    produce it). Raises ValueError when a record's trajectory is not that expansion of its step-0
+    row, bit for bit (such records must be sent whole)."""
+    N = horizon
+    recs = np.ascontiguousarray(recs, np.float32)
+    B = recs.shape[0]
+    out = np.zeros((B, compact_words(N)), np.float32)
+    out[:, :REC_HDR] = recs[:, :REC_HDR]
+    out[:, CREC_TRAJ0:CREC_TRAJ0 + 12] = recs[:, REC_HDR:REC_HDR + 12]
+    out[:, CREC_GAIT:CREC_GAIT + N] = recs[:, gait_offset(N):gait_offset(N) + N]
+    back = expand_records(out, N, dt)
+    bad = np.nonzero((back.view(np.uint32) != recs.view(np.uint32)).any(axis=1))[0]
+    if bad.size:
+        raise ValueError(f"{bad.size} records do not follow the controller's trajAll expansion "
+                         f"(first: {bad[0]}); send them as full records")
+    return out
+

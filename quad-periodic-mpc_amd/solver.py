@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "cmpc_batch_condense",
     "cmpc_batch_stream",
     "cmpc_last_error", "cmpc_batch_enable_timing", "cmpc_batch_enable_timing_every", "cmpc_batch_read_timing", "cmpc_batch_estimate",
-    "cmpc_batch_assemble", "cmpc_batch_rollout", "cmpc_batch_admm",
+    "cmpc_batch_assemble", "cmpc_batch_rollout", "cmpc_batch_admm", "cmpc_batch_expand",
     "cmpc_batch_quadprog",   # include/cmpc_quadprog.h
 )
 
@@ -100,6 +100,7 @@ def load_library(path: str = LIB_PATH):
                                     ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(AdmmSettings),
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.cmpc_batch_stream.argtypes = [ctypes.c_void_p]
+    lib.cmpc_batch_expand.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     lib.cmpc_batch_stream.restype = ctypes.c_void_p
     lib.cmpc_last_error.restype = ctypes.c_char_p
     lib.cmpc_batch_enable_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -329,6 +330,16 @@ class BatchSolver:
         _check(self.lib.cmpc_batch_assemble(self._h, _ptr(loco), ctypes.byref(loco_params),
                                             _ptr(records), _ptr(due), int(batch)),
                "cmpc_batch_assemble")
+
+    def expand(self, compact, records, batch: int | None = None) -> None:
+        """Compact records [B, CMPC_CREC_WORDS(N)] -> solve records [B, record_words] on device
+        (``cmpc_batch_expand``: trajAll from its step-0 row, ConvexMPCLocomotion.cpp:554-585)."""
+        if batch is None:
+            batch = compact.shape[0]
+        if hasattr(records, "shape"):
+            assert records.shape[-1] == self.record_words, "record stride mismatch"
+        _check(self.lib.cmpc_batch_expand(self._h, _ptr(compact), _ptr(records), int(batch)),
+               "cmpc_batch_expand")
 
     def rollout(self, loco, records, forces, xi6=None, due=None, batch: int | None = None) -> None:
         """One single-rigid-body MPC step of every due instance on device

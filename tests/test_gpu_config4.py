@@ -157,3 +157,36 @@ def test_root_pipeline_world2_gloo_real_solve(config4, tmp_path):
     assert results == {r: "ok" for r in range(world)}, results
     f_one, _ = _one_launch(solver_mod, prm, torch.from_numpy(recs).cuda())
     np.testing.assert_array_equal(np.load(out_path), f_one)
+
+
+def test_compact_records_expand_on_device_bitwise(cm, config4):
+    """cmpc_batch_expand (CMPC_CREC_* -> solve records, trajAll per ConvexMPCLocomotion.cpp:
+    554-585) reproduces the generator's records bit for bit at every horizon, and a world-1
+    RootPipeline over compact records gives the forces of the full ones."""
+    prm, recs, solver_mod = config4
+    R = importlib.import_module("quad-periodic-mpc_amd.records")
+    par = importlib.import_module("quad-periodic-mpc_amd.parallel")
+    for n in (1, 10, 16, 20):
+        p = cm.make_params(n)
+        full = cm.make_instances(5000, n, seed=61 + n, random_contact_frac=0.5)
+        comp = torch.from_numpy(R.compact_records(full, n, p.dt)).cuda()
+        out = torch.full((5000, R.record_words(n)), -7.0, dtype=torch.float32, device="cuda")
+        s = solver_mod.BatchSolver(p, max_batch=5000)
+        try:
+            s.expand(comp, out)
+            torch.cuda.synchronize()
+        finally:
+            s.close()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), full.view(np.uint32))
+    B = 40000
+    comp = torch.from_numpy(R.compact_records(recs[:B], N, prm.dt)).cuda()
+    f_one, st_one = _one_launch(solver_mod, prm, torch.from_numpy(recs[:B]).cuda())
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        pipe = par.RootPipeline(prm, B, chunks=2, device="cuda", record_format="compact")
+        pipe.step(comp)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(pipe.forces.cpu().numpy(), f_one)
+    np.testing.assert_array_equal(pipe.local_status.cpu().numpy(), st_one)
+    pipe.close()

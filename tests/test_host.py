@@ -78,16 +78,33 @@ def test_library_exports_header_symbols(cm):
     names = {line.split()[-1] for line in out.splitlines() if line.strip()}
     for sym in solver.EXPORTED_SYMBOLS:
         assert sym in names, sym
-    # every prototype in the header is among the exports
-    hdr = "".join(open(os.path.join(ROOT, "include", h)).read()
-                  for h in sorted(os.listdir(os.path.join(ROOT, "include"))) if h.endswith(".h"))
-    protos = re.findall(r"CMPC_EXTERNC\s+[\w\s\*]+?\b(\w+)\s*\(", hdr)
-    assert "cmpc_batch_quadprog" in protos
-    for p in protos:
-        assert p in names, p
+    # every prototype of a header is among the exports of its library (cmpc_multi.h:
+    # libcmpc_multi.so, the RCCL sharding; every other header: libcmpc_hip.so)
+    multi = os.path.join(os.path.dirname(path), "libcmpc_multi.so")
+    libs = {path: names}
+    if os.path.exists(multi):
+        mout = subprocess.run(["nm", "-D", "--defined-only", multi], capture_output=True, text=True,
+                              check=True).stdout
+        libs[multi] = {line.split()[-1] for line in mout.splitlines() if line.strip()}
+    seen = []
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if not h.endswith(".h"):
+            continue
+        protos = re.findall(r"CMPC_EXTERNC\s+[\w\s\*]+?\b(\w+)\s*\(", open(os.path.join(ROOT, "include", h)).read())
+        seen += protos
+        target = multi if h == "cmpc_multi.h" else path
+        if target not in libs:
+            pytest.fail(f"{target} not built")
+        for p in protos:
+            assert p in libs[target], (h, p)
+    assert "cmpc_batch_quadprog" in seen and "cmpc_multi_solve" in seen
     lib = ctypes.CDLL(path)  # loads without a GPU
     lib.cmpc_record_words.argtypes = [ctypes.c_int]
     assert lib.cmpc_record_words(10) == cm.record_words(10)
+    ml = ctypes.CDLL(multi)  # loads without a GPU (librccl resolved, nothing initialised)
+    ml.cmpc_multi_root_share.argtypes = [ctypes.c_int] * 3
+    ml.cmpc_multi_root_share.restype = ctypes.c_float
+    assert abs(ml.cmpc_multi_root_share(656, 481, 1) - (1 + 1137 / 3213.0)) < 1e-6
 
 
 def test_gait_tables_match_offset_duration_rule(cm):

@@ -91,8 +91,11 @@ def test_rank_sizes_root_share():
     """RootPipeline's plan: root keeps about root_share times a peer's rows (it solves them where
     they lie), the peers split the rest evenly, the blocks cover the batch in rank order."""
     par = importlib.import_module("quad-periodic-mpc_amd.parallel")
-    share = par.root_share_auto(164, 120)   # N = 10 records, every step's forces
-    assert 1.4 < share < 1.46
+    share = par.root_share_auto(164, 120)   # N = 10 records, every step's forces, one piece
+    assert 1.33 < share < 1.38
+    # two pieces: only half the transfer is exposed; compact records move 56 words, not 164
+    assert abs(par.root_share_auto(164, 120, 2) - 1 - (share - 1) / 2) < 1e-12
+    assert 1.18 < par.root_share_auto(56, 120) < 1.24
     for batch, world in ((262144, 8), (262144, 2), (10007, 3), (5, 4)):
         sizes = par.rank_sizes(batch, world, 0, share)
         assert sum(sizes) == batch and len(sizes) == world
@@ -112,7 +115,7 @@ def test_issue_order_interleaves():
                                   ("gather", 1), ("gather", 2)]
 
 
-def _pipe_worker(rank, world, port, batch, N, chunks, q):
+def _pipe_worker(rank, world, port, batch, N, chunks, q, record_format="full"):
     try:
         sys.path.insert(0, ROOT)
         import torch.distributed as dist
@@ -128,12 +131,17 @@ def _pipe_worker(rank, world, port, batch, N, chunks, q):
             forces.copy_(_fake_solve(recs[:, 32:], N))
             status.zero_()
 
-        pipe = par.RootPipeline(prm, batch, chunks=chunks, solve_fn=fn)
+        pipe = par.RootPipeline(prm, batch, chunks=chunks, solve_fn=fn, record_format=record_format)
+        held = full
+        if record_format == "compact":   # root holds the compact rows; every rank expands its own
+            R = importlib.import_module("quad-periodic-mpc_amd.records")
+            held = torch.from_numpy(R.compact_records(full.numpy(), N, prm.dt))
+            assert pipe.words == R.compact_words(N) and held.shape[1] == pipe.words
         if rank == 0:
             with pytest.raises(RuntimeError):
                 pipe.solve_only()   # root holds no records before its first step
         for _ in range(2):
-            pipe.step(full if rank == 0 else None)
+            pipe.step(held if rank == 0 else None)
         if rank == 0:
             assert torch.equal(pipe.forces, _fake_solve(full[:, 32:], N))
         log = pipe.op_log
@@ -168,3 +176,40 @@ def test_root_pipeline_pairwise_op_order(world, chunks):
         peer_seq = [(k, c) for k, c, peers in results[peer][1] if 0 in peers]
         assert root_seq == peer_seq, (peer, root_seq, peer_seq)
         assert len(peer_seq) == 2 * chunks
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 2)])
+def test_root_pipeline_compact_records(world, chunks):
+    """record_format="compact": root sends each peer the compact rows (trajAll's step-0 row, 56
+    words at N = 10 instead of 164) and every rank expands its own rows before the solve
+    (records.expand_records here, cmpc_batch_expand on a GPU): the gathered rows equal those of
+    the full records."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, 101, 10, chunks, q, "compact"))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v[0] == "ok" for v in results.values()), results
+
+
+def test_compact_records_roundtrip(cm):
+    """compact_records / expand_records: the generator's records (trajAll built as
+    ConvexMPCLocomotion.cpp:554-585 builds it) survive the round trip bit for bit at every
+    horizon; a record whose trajectory is not that expansion is refused."""
+    R = importlib.import_module("quad-periodic-mpc_amd.records")
+    for N in (1, 5, 10, 16, 20):
+        recs = cm.make_instances(257, N, seed=31 + N, random_contact_frac=0.5)
+        c = R.compact_records(recs, N, 0.026)
+        assert c.shape == (257, R.compact_words(N))
+        back = R.expand_records(c, N, 0.026)
+        np.testing.assert_array_equal(back.view(np.uint32), recs.view(np.uint32))
+    bad = recs.copy()
+    bad[3, R.REC_HDR + 12 * 4 + 5] += 0.01        # a height that is not the step-0 row's
+    with pytest.raises(ValueError):
+        R.compact_records(bad, 20, 0.026)
+
