@@ -221,6 +221,22 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                                           grid_of[1], ctx.side[1])
                         : hipSuccess;
     };
+    // The 120-column build (97..120; at N <= 13 almost always empty: all-stance tables only) on
+    // side 1: first, ahead of the 64-wide class-1 build and the 96 class, from round 6. Behind them
+    // its launch (a 14 us drain of its empty persistent grid at 32768 instances) was the last
+    // kernel of the step (profiles/r06_p/timeline). CMPC_W120_FIRST=0 (A/B): behind them.
+    static const int w120_env = diag_knob("CMPC_W120_SIDE", -1);
+    const int w120_side = (w120_env >= 0) ? (w120_env & 1) : (6 * P.N <= 80 ? 1 : 0);
+    static const int w120_skip = diag_knob("CMPC_SKIP_W120", 0);  // timing A/B only (n 97-120 unsolved)
+    static const int w120_first = diag_knob("CMPC_W120_FIRST", 1);
+    const bool w120_early = w120_first && w120_side == 1;
+    auto launch_w120 = [&]() -> hipError_t {
+      return (n_max > 96 && !w120_skip)
+                 ? launch_wide_w120(d_recs, P, d_forces, d_status, d_iters, list[8], &cnt[9], dq(8, 97, 120),
+                                    grid_of[8], ctx.side[w120_side])
+                 : hipSuccess;
+    };
+    if (w120_early && (e = launch_w120()) != hipSuccess) return e;
     if (w96_first && (e = launch_w96()) != hipSuccess) return e;
     // the 64-wide class-1 build over its list (60 < n <= 64), ahead of the wide classes on side 1
     // (side 0 carries the 80 class, the longest chain at N = 10)
@@ -237,12 +253,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // 96-column trot class at N = 14..16); below, on side 1 behind the sparse 96 class: at N = 10
     // its launch (few or no instances) otherwise lengthens side 0's 80-class chain, the step's
     // critical path (config 3 timeline, profiles/r04_prof). CMPC_W120_SIDE=0/1 forces a side (A/B)
-    static const int w120_env = diag_knob("CMPC_W120_SIDE", -1);
-    const int w120_side = (w120_env >= 0) ? (w120_env & 1) : (6 * P.N <= 80 ? 1 : 0);
-    static const int w120_skip = diag_knob("CMPC_SKIP_W120", 0);  // timing A/B only (n 97-120 unsolved)
-    if (n_max > 96 && !w120_skip && (e = launch_wide_w120(d_recs, P, d_forces, d_status, d_iters, list[8], &cnt[9],
-                                            dq(8, 97, 120), grid_of[8], ctx.side[w120_side])) != hipSuccess)
-      return e;
+    if (!w120_early && (e = launch_w120()) != hipSuccess) return e;
     if (n_max > 120 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
                                              dq(2, 121, 128), grid_of[2], ctx.side[1])) != hipSuccess)
       return e;
