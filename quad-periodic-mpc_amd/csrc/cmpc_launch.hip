@@ -222,13 +222,15 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                         : hipSuccess;
     };
     // The 120-column build (97..120; at N <= 13 almost always empty: all-stance tables only) on
-    // side 1: first, ahead of the 64-wide class-1 build and the 96 class, from round 6. Behind them
-    // its launch (a 14 us drain of its empty persistent grid at 32768 instances) was the last
-    // kernel of the step (profiles/r06_p/timeline). CMPC_W120_FIRST=0 (A/B): behind them.
+    // side 1 behind the 64-wide class-1 build and the 96 class. There its launch (a 14 us drain of
+    // its empty persistent grid at 32768 instances) is the last kernel of the step
+    // (profiles/r06_p), but ahead of them (CMPC_W120_FIRST=1, round 6) the drain waits for SIMD
+    // slots while class 1 fills the GPU and holds the 64-wide build and the 96 class back:
+    // 32768 instances -17 %, 65536 -14 %, 262144 -2 %, 4096 +0.3 % (profiles/r06_w120/ab.log).
     static const int w120_env = diag_knob("CMPC_W120_SIDE", -1);
     const int w120_side = (w120_env >= 0) ? (w120_env & 1) : (6 * P.N <= 80 ? 1 : 0);
     static const int w120_skip = diag_knob("CMPC_SKIP_W120", 0);  // timing A/B only (n 97-120 unsolved)
-    static const int w120_first = diag_knob("CMPC_W120_FIRST", 1);
+    static const int w120_first = diag_knob("CMPC_W120_FIRST", 0);
     const bool w120_early = w120_first && w120_side == 1;
     auto launch_w120 = [&]() -> hipError_t {
       return (n_max > 96 && !w120_skip)
