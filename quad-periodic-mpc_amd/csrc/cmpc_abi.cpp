@@ -250,6 +250,14 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
   e = hipEventCreateWithFlags(&h->ctx.fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.classified, hipEventDisableTiming);
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("fork event", e); }
+  // the class-count hint (cmpc_launch.hip): pinned, mapped, zero (no hint) until a classify pass
+  // copies a finished solve's header into it
+  e = hipHostMalloc(reinterpret_cast<void**>(&h->ctx.h_hint), sizeof(int) * cmpc::kHdr, hipHostMallocMapped);
+  if (e == hipSuccess) {
+    std::memset(h->ctx.h_hint, 0, sizeof(int) * cmpc::kHdr);
+    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&h->ctx.d_hint), h->ctx.h_hint, 0);
+  }
+  if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("hint buffer", e); }
   e = hipMalloc(&h->d_work, sizeof(int) * cmpc::work_ints(max_batch));
   if (e == hipSuccess) e = hipMemset(h->d_work, 0, sizeof(int) * 2 * cmpc::kHdr);  // both list headers
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("hipMalloc(work)", e); }
@@ -287,6 +295,8 @@ extern "C" void cmpc_batch_destroy(cmpc_batch* h) {
     if (h->ctx.join[j]) (void)hipEventDestroy(h->ctx.join[j]);
   if (h->ctx.fork) (void)hipEventDestroy(h->ctx.fork);
   if (h->ctx.classified) (void)hipEventDestroy(h->ctx.classified);
+  if (h->own_stream && h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->ctx.h_hint) (void)hipHostFree(h->ctx.h_hint);  // (the classify kernels writing it are done)
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }

@@ -64,7 +64,9 @@ struct LocoParams {
 constexpr int kLists = 11;
 constexpr int kHdr = 32;
 constexpr int kDeq = 16;  // cnt[kDeq + list]: dequeue counter of a persistent class's workgroups
-static_assert(1 + kLists <= kDeq && kDeq + kLists <= kHdr, "list lengths and dequeue counters fit the header");
+constexpr int kHdrBatch = 31;  // cnt[kHdrBatch]: the batch of the solve that counted into the header
+static_assert(1 + kLists <= kDeq && kDeq + kLists <= kHdrBatch && kHdrBatch < kHdr,
+              "list lengths, dequeue counters and the batch tag fit the header");
 inline size_t work_ints(int max_batch) { return 2 * kHdr + kLists * (size_t)max_batch; }
 // Side streams and events of one handle: the wider size classes run concurrently with class 1
 // (they are latency-bound: few instances, long serial solves). Three side streams (the third
@@ -80,6 +82,10 @@ struct LaunchCtx {
   hipEvent_t classified = nullptr;  // the classify pass (on side 0) is done
   hipEvent_t join[kSideStreams] = {nullptr, nullptr, nullptr};
   int hdr = 0;       // header (0 / 1) of d_work the next solve's lists count into
+  // class counts of an earlier solve (a header as the classify kernel left it, copied by a later
+  // classify pass): host-mapped pinned memory, read by launch_solve to size the wide classes' grids
+  int* h_hint = nullptr;
+  int* d_hint = nullptr;
   int last_hdr = 0;  // header of the last solve (its cnt[0] for cmpc_batch_read_timing)
 };
 // ev (optional): 3 events recorded on `stream`: ev[0] before class 1, ev[1] after it, ev[2]
@@ -95,7 +101,8 @@ hipError_t launch_class1(int nv, const float* d_recs, int batch, const KParams& 
 #define CMPC_DECL_WIDE(W)                                                                          \
   hipError_t launch_wide_w##W(const float* d_recs, const KParams& P, float* d_forces,             \
                               uint8_t* d_status, int32_t* d_iters, const int* in_list,            \
-                              const int* in_count, int* deq, int grid, hipStream_t stream);
+                              const int* in_count, int* deq, int grid, hipStream_t stream,     \
+                              int base = 0);
 CMPC_DECL_WIDE(80)
 CMPC_DECL_WIDE(96)
 CMPC_DECL_WIDE(120)
@@ -114,9 +121,11 @@ CMPC_DECL_WIDE(256)
 // kHandoffStatus (single-instance path: the host re-launches it in the wide class,
 // launch_single(..., allow_tail = false))
 constexpr uint8_t kHandoffStatus = 0xFE;
+// rest_grid > 0: `grid` covers the first entries only (a predicted count), and a looping kernel of
+// rest_grid workgroups follows on the stream for any entries past it
 hipError_t launch_tail(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
                        int32_t* d_iters, const int* in_list, const int* in_count, int* ovf_list,
-                       int* ovf_count, int grid, hipStream_t stream);
+                       int* ovf_count, int grid, hipStream_t stream, int rest_grid = 0);
 // the reduced sizes the tail class takes from the 80-column wide class: 64 < n <= 72 at N <= 10
 // (the horizons without the fp64 refinement of the wide classes; with the refinement switched
 // off, cmpc_batch_set_refine(0), the longer horizons keep the 80-column class, whose parity the

@@ -23,10 +23,17 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
                                                            KParams P, int* __restrict__ cnt,
                                                            int* __restrict__ lists, int max_batch,
                                                            int c1_max, int* __restrict__ next_hdr,
-                                                           int c1_listed, int tail) {
+                                                           int c1_listed, int tail,
+                                                           int* __restrict__ host_hint) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x < kHdr) next_hdr[threadIdx.x] = 0;  // the next solve's counters
+  if (blockIdx.x == 0 && threadIdx.x < kHdr) {
+    // the next solve's counters: before zeroing them, the previous solve's final counts (the
+    // header alternates) go to the host-mapped hint buffer (launch_solve sizes later grids by them)
+    if (host_hint) host_hint[threadIdx.x] = next_hdr[threadIdx.x];
+    next_hdr[threadIdx.x] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[kHdrBatch] = batch;  // this solve's batch: the hint's scale
   int cls = -1;
   if (i < batch) {
     const uint32_t* g =
@@ -81,6 +88,9 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
 // workgroups of the 80-column class's persistent launch over the tail class's hand-offs (an
 // active set past 64 positions: none in any measured workload; one workgroup solves them in turn)
 constexpr int kHandoffGrid = 1;
+// workgroups of the looping launch behind a one-per-entry launch of a predicted grid (entries past
+// the prediction; none when it held)
+constexpr int kRestGrid = 32;
 
 bool one_per_entry(int lo, int hi, int N, int batch) {
   static const int form = diag_knob("CMPC_WIDE_FORM", 0);
@@ -157,6 +167,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                            kHandoffGrid, s);
   };
   bool cls_side_used = false;
+  int tail_grid = batch;  // the tail class's grid (hinted below when the classify pass runs)
+  int tail_rest = 0;      // workgroups of its looping launch over entries past that grid
   if (n_max > 64) {
     // From 16384 instances (and up to 4096) the classify pass runs on side 0 beside class 1 (which
     // needs no list up to N = 10: it skips the instances above its row width itself), side 1
@@ -178,19 +190,47 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     }
     hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 63) / 64), dim3(64), 0, cs,
                        d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr, c1_listed ? 1 : 0,
-                       tail ? 1 : 0);
+                       tail ? 1 : 0, ctx.d_hint);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     ctx.last_hdr = ctx.hdr;
     if (!CMPC_HDR_MEMSET) ctx.hdr ^= 1;
     if ((e = hipEventRecord(ctx.classified, cs)) != hipSuccess) return e;
     for (int s = cls_side ? 1 : 0; s < nsides; s++)
       if ((e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
+    // launch form per wide class (cmpc_wide.h): one workgroup per entry for the class that holds
+    // the trot size n = 6N, persistent workgroups (dequeue counter) for the others
+    auto dq = [&](int lst, int lo, int hi) -> int* {
+      return one_per_entry(lo, hi, P.N, batch) ? nullptr : &cnt[kDeq + lst];
+    };
     int grid_of[kLists];
-    for (int j = 0; j < kLists; j++) grid_of[j] = batch;
-    // one workgroup per possible list entry (the lengths are only known on the device);
-    // surplus workgroups exit after one load. CMPC_EXACT_GRID=1 (diagnostic): read the list
-    // lengths back first (a host round trip per solve) and launch exact grids. Measured: +1 % at
-    // config 3, +0.2 % at config 5 (where the 256-row class launches only empty workgroups)
+    // Grids from the class counts of an earlier solve, from 16384 instances. The classify kernel
+    // copies a finished solve's header to the host-mapped ctx.h_hint (no host wait); scaled to
+    // this batch with a quarter and 64 workgroups of slack it sizes the wide classes' and the
+    // tail class's grids. A class launched one workgroup per possible entry ends only when its
+    // empty workgroups have drained, and at mid-size batches those wait for SIMD slots behind
+    // class 1: at 32768 instances the tail class and the 96 class ended 0.12-0.18 ms after class 1
+    // (profiles/r06_p). The persistent forms dequeue any count, so a hinted grid only bounds their
+    // workgroups; a one-per-entry launch over the predicted entries is followed on its stream by a
+    // small looping launch over any entries past them (kRestGrid workgroups of the class's
+    // persistent build, or the tail class's looping kernel), which exit at once when the
+    // prediction held. A class carrying the batch (N = 16's 96 class, N = 20's 120 class) predicts
+    // more than the batch and keeps a batch-sized grid; config 5's 128 class no longer launches
+    // 65536 workgroups for its few thousand instances. Below 16384 instances the drains are short and the grids stay batch-sized
+    // (a hint there measured +-0.3 %, profiles/r06_hint2). CMPC_HINT=0 (A/B): no hints.
+    static const int hint_env = diag_knob("CMPC_HINT", 1);
+    const volatile int* hint = (hint_env && ctx.h_hint && batch >= 16384) ? ctx.h_hint : nullptr;
+    const int hint_batch = hint ? hint[kHdrBatch] : 0;
+    const bool hinting = hint_batch > 0;
+    for (int j = 0; j < kLists; j++) {
+      grid_of[j] = batch;
+      if (!hinting) continue;
+      const double g = (double)hint[1 + j] * (double)batch / (double)hint_batch * 1.25 + 64.0;
+      if (g < (double)batch) grid_of[j] = (int)g;
+    }
+    grid_of[5] = grid_of[7] = batch;  // class-1 lists: their kernel takes one entry per workgroup
+    // CMPC_EXACT_GRID=1 (diagnostic): read this solve's list lengths back first (a host round
+    // trip per solve) and launch exact grids. Round 6 (profiles/r06_exact): 4096 instances -3 to
+    // -9 %, 32768 -2 to -4 %, 65536 -4 %, N = 16 +1.4 % — the host wait holds class 1's launch back
     static const bool exact = diag_knob("CMPC_EXACT_GRID", 0) == 1;
     if (exact) {
       static int* h_cnt = nullptr;
@@ -201,25 +241,33 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
         return e;
       for (int j = 0; j < kLists; j++) grid_of[j] = h_cnt[1 + j];
     }
-    // launch form per wide class (cmpc_wide.h): one workgroup per entry for the class that holds
-    // the trot size n = 6N, persistent workgroups (dequeue counter) for the others
-    auto dq = [&](int lst, int lo, int hi) -> int* {
-      return one_per_entry(lo, hi, P.N, batch) ? nullptr : &cnt[kDeq + lst];
+    const bool rest = hinting && !exact;  // entries past a predicted grid are possible
+    tail_grid = grid_of[9];
+    tail_rest = rest && tail_grid < batch ? kRestGrid : 0;
+    // one wide class: persistent (hinted grid) or one-per-entry (+ the rest launch behind it)
+    using WideFn = hipError_t (*)(const float*, const KParams&, float*, uint8_t*, int32_t*, const int*,
+                                  const int*, int*, int, hipStream_t, int);
+    auto wide = [&](WideFn fn, int lst, int lo, int hi, hipStream_t s) -> hipError_t {
+      int* d = dq(lst, lo, hi);
+      if (d) return fn(d_recs, P, d_forces, d_status, d_iters, list[lst], &cnt[1 + lst], d, grid_of[lst], s, 0);
+      const int g = grid_of[lst];
+      hipError_t r = fn(d_recs, P, d_forces, d_status, d_iters, list[lst], &cnt[1 + lst], nullptr, g, s, 0);
+      if (r != hipSuccess || !rest || g >= batch) return r;
+      return fn(d_recs, P, d_forces, d_status, d_iters, list[lst], &cnt[1 + lst], &cnt[kDeq + lst], kRestGrid, s,
+                g);
     };
     // the tail class first on side 0 / side 2 (t8_pos above), its hand-offs (list 10) to the
     // 80-column class right behind it on the same stream
     if (tail && (t8_pos == 0 || t8_pos == 2) &&
         ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11],
-                          grid_of[9], ctx.side[t8_pos])) != hipSuccess ||
+                          grid_of[9], ctx.side[t8_pos], tail_rest)) != hipSuccess ||
          (e = launch_handoff(ctx.side[t8_pos])) != hipSuccess))
       return e;
     // CMPC_W96_FIRST (diagnostic A/B): the 96-column class ahead of the 64-wide class-1 build on
     // side 1 (its few long solves start at once instead of behind that build)
     static const int w96_first = diag_knob("CMPC_W96_FIRST", 0);
     auto launch_w96 = [&]() -> hipError_t {
-      return n_max > 80 ? launch_wide_w96(d_recs, P, d_forces, d_status, d_iters, list[1], &cnt[2], dq(1, 81, 96),
-                                          grid_of[1], ctx.side[1])
-                        : hipSuccess;
+      return n_max > 80 ? wide(launch_wide_w96, 1, 81, 96, ctx.side[1]) : hipSuccess;
     };
     // The 120-column build (97..120; at N <= 13 almost always empty: all-stance tables only) on
     // side 1 behind the 64-wide class-1 build and the 96 class. There its launch (a 14 us drain of
@@ -234,8 +282,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     const bool w120_early = w120_first && w120_side == 1;
     auto launch_w120 = [&]() -> hipError_t {
       return (n_max > 96 && !w120_skip)
-                 ? launch_wide_w120(d_recs, P, d_forces, d_status, d_iters, list[8], &cnt[9], dq(8, 97, 120),
-                                    grid_of[8], ctx.side[w120_side])
+                 ? wide(launch_wide_w120, 8, 97, 120, ctx.side[w120_side])
                  : hipSuccess;
     };
     if (w120_early && (e = launch_w120()) != hipSuccess) return e;
@@ -247,18 +294,14 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
       return e;
     // side 0: 80, 120, 144, 256; side 1: 96, 128, 192 (at N = 20 the 120-column class, which
     // carries the batch, runs beside the 128-column class)
-    if ((e = launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[0], &cnt[1],
-                             dq(0, 65, 80), grid_of[0], ctx.side[0])) != hipSuccess)
-      return e;
+    if ((e = wide(launch_wide_w80, 0, 65, 80, ctx.side[0])) != hipSuccess) return e;
     if (!w96_first && (e = launch_w96()) != hipSuccess) return e;
     // the 120-column build on side 0 from N = 14 (every trot instance at N = 17..20, beside the
     // 96-column trot class at N = 14..16); below, on side 1 behind the sparse 96 class: at N = 10
     // its launch (few or no instances) otherwise lengthens side 0's 80-class chain, the step's
     // critical path (config 3 timeline, profiles/r04_prof). CMPC_W120_SIDE=0/1 forces a side (A/B)
     if (!w120_early && (e = launch_w120()) != hipSuccess) return e;
-    if (n_max > 120 && (e = launch_wide_w128(d_recs, P, d_forces, d_status, d_iters, list[2], &cnt[3],
-                                             dq(2, 121, 128), grid_of[2], ctx.side[1])) != hipSuccess)
-      return e;
+    if (n_max > 120 && (e = wide(launch_wide_w128, 2, 121, 128, ctx.side[1])) != hipSuccess) return e;
     // The 144 class on side 0 behind the 120 class, the 192 class on side 1 behind the 128 class:
     // at N = 20 the two sparse classes then start as soon as either bulk class drains and run side
     // by side instead of back to back. Config 5 4.21 M -> 4.41 M QP/s against both on side 1
@@ -278,8 +321,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   }
   if (tail_on && t8_pos == 3) {  // the tail class ahead of class 1 on the handle's stream
     if (cls_side_used && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
-    if ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11], batch,
-                         stream)) != hipSuccess ||
+    if ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11], tail_grid,
+                         stream, tail_rest)) != hipSuccess ||
         (e = launch_handoff(stream)) != hipSuccess)
       return e;
   }
@@ -299,8 +342,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   if (e != hipSuccess) return e;
   if (tail_on && t8_pos == 1) {  // the tail class behind class 1 on the handle's stream
     if (cls_side_used && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
-    if ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11], batch,
-                         stream)) != hipSuccess ||
+    if ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11], tail_grid,
+                         stream, tail_rest)) != hipSuccess ||
         (e = launch_handoff(stream)) != hipSuccess)
       return e;
   }

@@ -965,31 +965,53 @@ __device__ __forceinline__ void solve_t(const float* __restrict__ rec, const KPa
 
 }  // namespace
 
-// One workgroup per possible list entry (the list length is only known on the device); surplus
-// workgroups exit after reading the count. (A persistent form that dequeues the list measured
-// worse everywhere: its resident 168-VGPR waves keep two class-1 waves off every SIMD they share
-// for the whole run, profiles/r05_h, r05_i.)
+// One workgroup per list entry (entries first + blockIdx.x). The grid covers the whole list
+// (one workgroup per possible entry: surplus workgroups exit after reading the count) or, from
+// 16384 instances, the count an earlier solve predicts (cmpc_launch.hip hint), followed by the
+// looping form below over any entries past it. (A persistent form that dequeues the whole list
+// measured worse everywhere: its resident 168-VGPR waves keep two class-1 waves off every SIMD
+// they share for the whole run, profiles/r05_h, r05_i; a grid-stride loop in this kernel itself
+// spills 24 B more and cost 4-6 % at 4096 instances, profiles/r06_hint2.)
 __global__ __launch_bounds__(64, CMPC_TAIL_WAVES_PER_EU) void cmpc_solve_t_kernel(
     const float* __restrict__ recs, KParams P, float* __restrict__ forces, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, const int* __restrict__ in_list, const int* __restrict__ in_count,
-    int* __restrict__ ovf_list, int* __restrict__ ovf_count) {
+    int* __restrict__ ovf_list, int* __restrict__ ovf_count, int first) {
   __shared__ SharedT<kTailRows> sh;
 #if CMPC_TAIL_PRIO > 0
   __builtin_amdgcn_s_setprio(CMPC_TAIL_PRIO);
 #endif
-  const int b = blockIdx.x;
+  const int b = first + (int)blockIdx.x;
   if (b >= *in_count) return;
   const int t = in_list[b];
   solve_t<kTailRows>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * P.out_cols, status + t,
                      iters ? iters + t : nullptr, ovf_list, ovf_count, t);
 }
 
+// The entries past a predicted grid (normally none: its few workgroups exit at once), grid-stride.
+__global__ __launch_bounds__(64, CMPC_TAIL_WAVES_PER_EU) void cmpc_solve_t_rest_kernel(
+    const float* __restrict__ recs, KParams P, float* __restrict__ forces, uint8_t* __restrict__ status,
+    int32_t* __restrict__ iters, const int* __restrict__ in_list, const int* __restrict__ in_count,
+    int* __restrict__ ovf_list, int* __restrict__ ovf_count, int first) {
+  __shared__ SharedT<kTailRows> sh;
+  const int count = *in_count;
+  for (int b = first + (int)blockIdx.x; b < count; b += (int)gridDim.x) {
+    const int t = in_list[b];
+    solve_t<kTailRows>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * P.out_cols, status + t,
+                       iters ? iters + t : nullptr, ovf_list, ovf_count, t);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
 hipError_t launch_tail(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
                        int32_t* d_iters, const int* in_list, const int* in_count, int* ovf_list,
-                       int* ovf_count, int grid, hipStream_t stream) {
+                       int* ovf_count, int grid, hipStream_t stream, int rest_grid) {
   if (grid <= 0) return hipSuccess;
   hipLaunchKernelGGL(cmpc_solve_t_kernel, dim3(grid), dim3(64), 0, stream, d_recs, P, d_forces, d_status, d_iters,
-                     in_list, in_count, ovf_list, ovf_count);
+                     in_list, in_count, ovf_list, ovf_count, 0);
+  if (rest_grid > 0)
+    hipLaunchKernelGGL(cmpc_solve_t_rest_kernel, dim3(rest_grid), dim3(64), 0, stream, d_recs, P, d_forces,
+                       d_status, d_iters, in_list, in_count, ovf_list, ovf_count, grid);
   return hipGetLastError();
 }
 

@@ -1508,6 +1508,7 @@ struct WideArgs {
   const int* in_count;
   int* deq;
   KParams P;
+  int base;  // persistent form: first list entry it takes (0, or the grid of a one-per-entry launch)
 };
 
 // REFINE is part of the kernel's name: the refining and plain builds of a class live in different
@@ -1530,7 +1531,9 @@ __global__ __launch_bounds__(WGeo<NV>::NT, CMPC_WIDE_WAVES_PER_EU) CMPC_WIDE_VGP
   } else {
     for (int round = 0;; round++) {
       // deq == nullptr (single-instance path): workgroup i takes entry i, once
-      if (threadIdx.x == 0) sh.deq_b = A.deq ? atomicAdd(A.deq, 1) : (round == 0 ? (int)blockIdx.x : count);
+      // base: entries below it belong to a one-per-entry launch of a predicted grid (this launch
+      // takes the rest, cmpc_launch.hip hint); 0 otherwise
+      if (threadIdx.x == 0) sh.deq_b = A.base + (A.deq ? atomicAdd(A.deq, 1) : (round == 0 ? (int)blockIdx.x : count));
       wbar();
       const int b = __builtin_amdgcn_readfirstlane(sh.deq_b);
       if (b >= count) break;
@@ -1566,11 +1569,11 @@ namespace {
 template <int NV>
 hipError_t launch_wide_impl(const float* d_recs, const KParams& P, float* d_forces,
                             uint8_t* d_status, int32_t* d_iters, const int* in_list,
-                            const int* in_count, int* deq, int grid, hipStream_t stream) {
+                            const int* in_count, int* deq, int grid, hipStream_t stream, int base = 0) {
   if (grid <= 0) return hipSuccess;
   constexpr bool kOne = (CMPC_WIDE_BUILD & 1) != 0, kPersist = (CMPC_WIDE_BUILD & 2) != 0;
   const bool persist = kPersist && (deq != nullptr || !kOne);
-  WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, in_count, persist ? deq : nullptr, P};
+  WideArgs A{d_recs, d_forces, d_status, d_iters, in_list, in_count, persist ? deq : nullptr, P, base};
   if (persist) {
     if constexpr (kPersist) {
       constexpr bool kRef = CMPC_WIDE_REFINE != 0;

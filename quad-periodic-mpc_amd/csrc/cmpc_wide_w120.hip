@@ -21,22 +21,22 @@ namespace cmpc {
 // the same class with the fp64 refinement step (N > 10), each launch form in its own unit
 hipError_t launch_wide_w120_r(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
                             int32_t* d_iters, const int* in_list, const int* in_count, int* deq, int grid,
-                            hipStream_t stream);
+                            hipStream_t stream, int base);
 hipError_t launch_wide_w120_persist_r(const float* d_recs, const KParams& P, float* d_forces,
                                     uint8_t* d_status, int32_t* d_iters, const int* in_list,
-                                    const int* in_count, int* deq, int grid, hipStream_t stream);
+                                    const int* in_count, int* deq, int grid, hipStream_t stream, int base);
 
 hipError_t launch_wide_w120(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
                           int32_t* d_iters, const int* in_list, const int* in_count, int* deq, int grid,
-                          hipStream_t stream) {
+                          hipStream_t stream, int base) {
   if (P.refine)
-    return deq ? launch_wide_w120_persist_r(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid, stream)
-               : launch_wide_w120_r(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, nullptr, grid, stream);
+    return deq ? launch_wide_w120_persist_r(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid, stream, base)
+               : launch_wide_w120_r(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, nullptr, grid, stream, base);
   if (deq)  // persistent form: its own unit (compiled beside this kernel it spilled registers)
     return launch_wide_w120_persist(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid,
-                                   stream);
+                                   stream, base);
   return launch_wide_impl<120>(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, nullptr, grid,
-                              stream);
+                              stream, base);
 }
 
 }  // namespace cmpc

@@ -13,12 +13,12 @@ namespace cmpc {
 
 hipError_t launch_wide_w128(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
                           int32_t* d_iters, const int* in_list, const int* in_count, int* deq, int grid,
-                          hipStream_t stream) {
+                          hipStream_t stream, int base) {
   if (deq)  // persistent form: its own unit (compiled beside this kernel it spilled registers)
     return launch_wide_w128_persist(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid,
-                                   stream);
+                                   stream, base);
   return launch_wide_impl<128>(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, nullptr, grid,
-                              stream);
+                              stream, base);
 }
 
 }  // namespace cmpc

@@ -6,9 +6,9 @@ namespace cmpc {
 
 hipError_t launch_wide_w256(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
                           int32_t* d_iters, const int* in_list, const int* in_count, int* deq, int grid,
-                          hipStream_t stream) {
+                          hipStream_t stream, int base) {
   return launch_wide_impl<256>(d_recs, P, d_forces, d_status, d_iters, in_list, in_count, deq, grid,
-                              stream);
+                              stream, base);
 }
 
 }  // namespace cmpc

@@ -626,3 +626,31 @@ def test_output_steps_keep_leading_forces_bitwise(cm, solver_mod, N, steps):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(pipe.forces.cpu().numpy(), f_full[:, :oc])
     pipe.close()
+
+
+@pytest.mark.parametrize("N,B", [(10, 4096), (10, 32768), (20, 16384)])
+def test_stale_grid_hint_still_solves_every_instance(cm, solver_mod, N, B):
+    """The wide and tail classes size their grids from an earlier solve's class counts
+    (cmpc_launch.hip hint). A handle that solved trot-only batches (few or no instances above
+    class 1: the hint says ~0) then gets a random-contact batch of the same size (thousands of
+    them): the one-per-entry grids grid-stride and the persistent ones dequeue past the hinted
+    size, so every instance is solved, bit for bit as by a fresh handle; and back again."""
+    prm = cm.make_params(N)
+    trot = cm.make_instances(B, N, seed=9700 + N, random_contact_frac=0.0)
+    mixed = cm.make_instances(B, N, seed=9800 + N, random_contact_frac=1.0)
+    s = solver_mod.BatchSolver(prm, max_batch=B)
+    try:
+        for _ in range(3):
+            s.solve_host(trot)
+        got = [s.solve_host(mixed) for _ in range(3)]
+        back = s.solve_host(trot)
+    finally:
+        s.close()
+    f_ref, st_ref, it_ref = gpu_solve(solver_mod, prm, mixed)
+    t_ref = gpu_solve(solver_mod, prm, trot)
+    assert (st_ref == 0).all(), np.bincount(st_ref)
+    for f, st, it in got:
+        np.testing.assert_array_equal(f, f_ref)
+        np.testing.assert_array_equal(st, st_ref)
+        np.testing.assert_array_equal(it, it_ref)
+    np.testing.assert_array_equal(back[0], t_ref[0])
