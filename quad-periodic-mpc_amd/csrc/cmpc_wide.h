@@ -1444,25 +1444,31 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
     wbar();
     for (int i = t; i < 12 * N; i += G::NT) sh.P[i] = 0.f;
     wbar();
-    if (ok && h == 0 && r < n) sh.P[12 * sh.varblk[r] + sh.varcol[r]] = xv;
-    wbar();
     // A stance foot-step whose own working-set rows pin all three forces (a vertex of its
     // pyramid: fz = 0 or fz = ub, or two opposite faces, with fx and fy each on a face) takes them
     // from those rows exactly. The fp32 steps of the active set leave x there at ~1e-6 of the
     // unconstrained minimiser: on an all-zero vertex reached from hundreds of N that was 4e-4 N
-    // (the tail class's hand-offs, tests/test_gpu_parity.py), beyond 1e-4 x max(|f|, 1 N).
-    if (ok && t < nfs) {
-      const unsigned char* cf = &sh.cflag[6 * t];
-      const bool z0 = cf[4] || (cf[0] && cf[1]) || (cf[2] && cf[3]);
-      if ((z0 || cf[5]) && (cf[0] || cf[1]) && (cf[2] || cf[3])) {
-        const float fz = z0 ? 0.f : sh.sub[t];
-        const float fxy = fz / mui;  // +-mui f + fz = 0 on an active face
-        const float fx = z0 ? 0.f : (cf[0] ? -fxy : fxy);
-        const float fy = z0 ? 0.f : (cf[2] ? -fxy : fxy);
-        sh.P[12 * sh.varblk[3 * t] + sh.varcol[3 * t]] = fx;
-        sh.P[12 * sh.varblk[3 * t + 1] + sh.varcol[3 * t + 1]] = fy;
-        sh.P[12 * sh.varblk[3 * t + 2] + sh.varcol[3 * t + 2]] = fz;
+    // (the tail class's hand-offs, tests/test_gpu_parity.py), beyond 1e-4 x max(|f|, 1 N). Each
+    // variable's thread decides for its own component.
+    if (ok && h == 0 && r < n) {
+      const int fs = r / 3, ax = r - 3 * fs;
+      // the foot-step's six flags as one 4-byte and one 2-byte load (six byte loads here had the
+      // refining wide 96 build spill 12 B more)
+      unsigned int f4;
+      unsigned short f2;
+      __builtin_memcpy(&f4, &sh.cflag[6 * fs], 4);
+      __builtin_memcpy(&f2, &sh.cflag[6 * fs + 4], 2);
+      const bool c0 = f4 & 0xffu, c1 = f4 & 0xff00u, c2 = f4 & 0xff0000u, c3 = f4 & 0xff000000u;
+      const bool c4 = f2 & 0xffu, c5 = f2 & 0xff00u;
+      const bool z0 = c4 || (c0 && c1) || (c2 && c3);
+      float out = xv;
+      if ((z0 || c5) && (c0 || c1) && (c2 || c3)) {
+        const float fz = z0 ? 0.f : sh.sub[fs];
+        const float fxy = wdiv(vopq(fz), sopq(P.mu_inv));  // +-mui f + fz = 0 on an active face
+        const bool neg = (ax == 0) ? c0 : c2;
+        out = (ax == 2) ? fz : (z0 ? 0.f : (neg ? -fxy : fxy));
       }
+      sh.P[12 * sh.varblk[r] + sh.varcol[r]] = out;
     }
     wbar();
     for (int i = 4 * t; i < P.out_cols; i += 4 * G::NT)  // (the leading steps kept, 12 N by default)
