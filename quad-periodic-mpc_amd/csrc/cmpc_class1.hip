@@ -37,6 +37,14 @@
 #ifndef CMPC_C1_RL
 #define CMPC_C1_RL 0
 #endif
+// Active-set trips after which a wave raises its issue priority (0: never): the instances with
+// many trips set the end of a batch that does not fill the GPU many times over
+#ifndef CMPC_TRIP_PRIO_AT
+#define CMPC_TRIP_PRIO_AT 0
+#endif
+#ifndef CMPC_C1_TRIP_PRIO
+#define CMPC_C1_TRIP_PRIO 2
+#endif
 // chunks per group of the software-pipelined vector sweeps (piped_sweep)
 #ifndef C1_PIPE_GRP
 #define C1_PIPE_GRP 4
@@ -601,6 +609,10 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       }
       C1_SUB(0);
       if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
+#if CMPC_TRIP_PRIO_AT > 0
+      // a long solve: issue ahead of the other waves on this SIMD (shorter makespan tail)
+      if (iters == CMPC_TRIP_PRIO_AT) __builtin_amdgcn_s_setprio(CMPC_C1_TRIP_PRIO);
+#endif
       // d = J' n+ : rows ia, iz of J through LDS (dword stores: wide stores would tie the row
       // registers into tuples)
       if (v == cp.ia || v == cp.iz) {  // both rows in one pass (two lanes per store)

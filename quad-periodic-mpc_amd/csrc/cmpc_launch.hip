@@ -154,10 +154,22 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   static const int tail_env = diag_knob("CMPC_TAIL", 1);
   const bool tail = tail_env != 0 && tail_class(P, 65);
   const bool tail_on = tail && n_max > 64;
+  // CMPC_WIDE_FIRST (A/B, N <= 10): the classify pass first on the handle's stream, the tail and
+  // wide classes (hinted grids) launched on their side streams ahead of class 1, so their long
+  // solves take SIMD slots before class 1's waves fill the GPU; 2: class 1 over its classify list
+  static const int wf_env = diag_knob("CMPC_WIDE_FIRST", 0);
+  const bool wide_first = wf_env > 0 && !c1_listed && n_max > 64;
+  const bool c1_list_mode = c1_listed || (wide_first && wf_env == 2);
   static const int t8_env = diag_knob("CMPC_T8_POS", -1);
-  const int t8_pos = (t8_env >= 0) ? t8_env : (batch >= 131072 ? 1 : 2);
+  const int t8_pos = (t8_env >= 0) ? t8_env : ((batch >= 131072 && !wide_first) ? 1 : 2);
   // side streams forked and joined by this solve (the third only for the tail class's own chain)
   const int nsides = (tail && t8_pos == 2) ? 3 : 2;
+  // CMPC_C1_SIDE=1 (A/B, N <= 10 with the tail class on side 2): class 1 and the tail class swap
+  // streams — class 1 (which ends first at small batches) on side 2, the tail class on the
+  // handle's stream behind the classify pass — so the join waits on queues that are already idle
+  static const int c1side_env = diag_knob("CMPC_C1_SIDE", 0);
+  const bool c1_swap = c1side_env == 1 && tail_on && t8_pos == 2 && !c1_list_mode;
+  hipStream_t c1_stream = c1_swap ? ctx.side[2] : stream;
   // the tail class's hand-offs, behind it on its stream: a one-workgroup persistent launch of the
   // 80-column class (it reads the final count once the tail class is done)
   static const int handoff_env = diag_knob("CMPC_HANDOFF", 1);  // 0: no hand-off launch (timing A/B only)
@@ -181,22 +193,24 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // Round-4 sweep (profiles/r04_ab/r04_ks, beside vs ahead): 2048 +2.3 %, 4096 (config 2)
     // +3.2 %, 6144 0, 8192 -2 %, 12288 -1.5 %: beside at the smallest batches too, where class 1
     // starting without the classify pass's queue hop ahead of it pays most
-    const bool cls_side = (cls_env < 0) ? (batch >= 16384 || batch <= 4096) : (cls_env == 1);
+    const bool cls_side = c1_swap ? true : wide_first ? false : (cls_env < 0) ? (batch >= 16384 || batch <= 4096) : (cls_env == 1);
     cls_side_used = cls_side;
     hipStream_t cs = cls_side ? ctx.side[0] : stream;
     if (cls_side) {
       if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(ctx.side[0], ctx.fork, 0)) != hipSuccess) return e;
+      if (c1_swap && (e = hipStreamWaitEvent(ctx.side[2], ctx.fork, 0)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 63) / 64), dim3(64), 0, cs,
-                       d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr, c1_listed ? 1 : 0,
+                       d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr, c1_list_mode ? 1 : 0,
                        tail ? 1 : 0, ctx.d_hint);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     ctx.last_hdr = ctx.hdr;
     if (!CMPC_HDR_MEMSET) ctx.hdr ^= 1;
     if ((e = hipEventRecord(ctx.classified, cs)) != hipSuccess) return e;
     for (int s = cls_side ? 1 : 0; s < nsides; s++)
-      if ((e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
+      if (!(c1_swap && s == 2) && (e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
+    if (c1_swap && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
     // launch form per wide class (cmpc_wide.h): one workgroup per entry for the class that holds
     // the trot size n = 6N, persistent workgroups (dequeue counter) for the others
     auto dq = [&](int lst, int lo, int hi) -> int* {
@@ -218,7 +232,8 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // 65536 workgroups for its few thousand instances. Below 16384 instances the drains are short and the grids stay batch-sized
     // (a hint there measured +-0.3 %, profiles/r06_hint2). CMPC_HINT=0 (A/B): no hints.
     static const int hint_env = diag_knob("CMPC_HINT", 1);
-    const volatile int* hint = (hint_env && ctx.h_hint && batch >= 16384) ? ctx.h_hint : nullptr;
+    static const int hint_min = diag_knob("CMPC_HINT_MIN", 16384);
+    const volatile int* hint = (hint_env && ctx.h_hint && batch >= hint_min) ? ctx.h_hint : nullptr;
     const int hint_batch = hint ? hint[kHdrBatch] : 0;
     const bool hinting = hint_batch > 0;
     for (int j = 0; j < kLists; j++) {
@@ -258,10 +273,11 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     };
     // the tail class first on side 0 / side 2 (t8_pos above), its hand-offs (list 10) to the
     // 80-column class right behind it on the same stream
+    hipStream_t t8_stream = c1_swap ? stream : ctx.side[(t8_pos == 0 || t8_pos == 2) ? t8_pos : 0];
     if (tail && (t8_pos == 0 || t8_pos == 2) &&
         ((e = launch_tail(d_recs, P, d_forces, d_status, d_iters, list[9], &cnt[10], list[10], &cnt[11],
-                          grid_of[9], ctx.side[t8_pos], tail_rest)) != hipSuccess ||
-         (e = launch_handoff(ctx.side[t8_pos])) != hipSuccess))
+                          grid_of[9], t8_stream, tail_rest)) != hipSuccess ||
+         (e = launch_handoff(t8_stream)) != hipSuccess))
       return e;
     // CMPC_W96_FIRST (diagnostic A/B): the 96-column class ahead of the 64-wide class-1 build on
     // side 1 (its few long solves start at once instead of behind that build)
@@ -326,10 +342,10 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
         (e = launch_handoff(stream)) != hipSuccess)
       return e;
   }
-  if (ev) (void)hipEventRecord(ev[0], stream);
+  if (ev) (void)hipEventRecord(ev[0], c1_stream);
   // class 1: up to N = 10 over the whole batch (it skips the instances above its row width
   // itself), from N = 11 over list 5
-  if (c1_listed) {
+  if (c1_list_mode) {
     // class 1 over the classify list of n <= its row width (one workgroup per possible entry,
     // surplus ones exit after reading the count): behind the classify pass
     if (cls_side_used && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
@@ -337,7 +353,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
                       nullptr, batch, stream);
   } else {
     e = launch_class1(c1_nv, d_recs, batch, P, d_forces, d_status, d_iters, nullptr, nullptr, nullptr,
-                      nullptr, batch, stream);
+                      nullptr, batch, c1_stream);
   }
   if (e != hipSuccess) return e;
   if (tail_on && t8_pos == 1) {  // the tail class behind class 1 on the handle's stream
@@ -347,7 +363,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
         (e = launch_handoff(stream)) != hipSuccess)
       return e;
   }
-  if (ev) (void)hipEventRecord(ev[1], stream);
+  if (ev) (void)hipEventRecord(ev[1], c1_stream);
   if (n_max > 64) {
     for (int s = 0; s < nsides; s++) {
       if ((e = hipEventRecord(ctx.join[s], ctx.side[s])) != hipSuccess) return e;

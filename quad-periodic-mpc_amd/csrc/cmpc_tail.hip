@@ -29,6 +29,12 @@
 #ifndef CMPC_TAIL_WAVES_PER_EU
 #define CMPC_TAIL_WAVES_PER_EU 3
 #endif
+#ifndef CMPC_TRIP_PRIO_AT  // active-set trips after which a wave raises its priority (0: never)
+#define CMPC_TRIP_PRIO_AT 0
+#endif
+#ifndef CMPC_TAIL_TRIP_PRIO
+#define CMPC_TAIL_TRIP_PRIO 3
+#endif
 #ifndef CMPC_TAIL_PRIO  // s_setprio of the tail classes' waves: issue ahead of the class-1 waves on their SIMDs
 #define CMPC_TAIL_PRIO 1
 #endif
@@ -677,6 +683,9 @@ __device__ __forceinline__ void solve_t(const float* __restrict__ rec, const KPa
         up = 0.f;
       }
       if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
+#if CMPC_TRIP_PRIO_AT > 0
+      if (iters == CMPC_TRIP_PRIO_AT) __builtin_amdgcn_s_setprio(CMPC_TAIL_TRIP_PRIO);
+#endif
       // d = J' n+: rows ia, iz of J through LDS (main rows from their lanes, tail rows from their
       // segments)
       if (v == cp.ia || v == cp.iz) {

@@ -55,6 +55,12 @@
 #define CMPC_WIDE_REFINE 1
 #endif
 // refinements per instance at most, and the constraint tolerance (x x_max) after one
+#ifndef CMPC_TRIP_PRIO_AT  // active-set trips after which the N <= 10 builds raise their priority
+#define CMPC_TRIP_PRIO_AT 0
+#endif
+#ifndef CMPC_WIDE_TRIP_PRIO
+#define CMPC_WIDE_TRIP_PRIO 3
+#endif
 #ifndef CMPC_WIDE_PRIO  // s_setprio of the wide classes' waves (0: the default priority)
 #define CMPC_WIDE_PRIO 0
 #endif
@@ -1057,6 +1063,9 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
         up = 0.f;
       }
       if (++iters > P.max_iter + 2 * n) { status = CMPC_MAX_ITER; break; }
+#if CMPC_WIDE_PRIO > 0 && CMPC_TRIP_PRIO_AT > 0
+      if (iters == CMPC_TRIP_PRIO_AT) __builtin_amdgcn_s_setprio(CMPC_WIDE_TRIP_PRIO);
+#endif
       // d = J' n+ : rows ia, iz of J through LDS (logical order)
       if (r == cp.ia && cp.ia != cp.iz) {
 #pragma unroll

@@ -2,15 +2,17 @@
 # Same-box A/B of library builds: each workload timed under every CMPC_LIB in turn, the whole
 # rotation repeated (ABAB...), so drift over the session hits every build alike.
 # usage: scripts/gpu_lib_ab.sh <tag> <reps> default variants/a.so variants/b.so ...
-# workloads: config 3, config 2, N = 16 trot, config 5 (bench.py --no-extras, one line each)
+# workloads: config 3, config 2, N = 16 trot, config 5 (bench.py --no-extras, one line each);
+# WL="cfg3 b32768 ..." picks others (bNNN: config 3's mix at batch NNN)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=$1; REPS=$2; shift 2
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 for rep in $(seq 1 "$REPS"); do
-  for w in cfg3 cfg2 n16 cfg5; do
+  for w in ${WL:-cfg3 cfg2 n16 cfg5}; do
     case $w in
+      b*) args="--config 3 --batch ${w#b} --steps 50" ;;
       cfg3) args="--config 3 --steps 50" ;;
       cfg2) args="--config 2 --steps 200" ;;
       n16) args="--horizon 16 --random-contact-frac 0 --steps 20" ;;
