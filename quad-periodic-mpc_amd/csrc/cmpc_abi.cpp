@@ -243,12 +243,17 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
     for (int j = 0; j < cmpc::kSideStreams; j++) h->ctx.side[j] = sides[j];
     h->pooled_sides = true;
   }
+  // CMPC_EVENT_SCOPE (A/B): the fork / classified / join events' release scope: 0 the default
+  // (system scope), 1 device scope, 2 no system fence (every consumer is a queue of this device)
+  const int ev_scope = cmpc::diag_knob("CMPC_EVENT_SCOPE", 0);
+  const unsigned ev_flags = hipEventDisableTiming | (ev_scope == 1 ? hipEventReleaseToDevice
+                                                     : ev_scope == 2 ? hipEventDisableSystemFence : 0u);
   for (int j = 0; j < cmpc::kSideStreams; j++) {
-    e = hipEventCreateWithFlags(&h->ctx.join[j], hipEventDisableTiming);
+    e = hipEventCreateWithFlags(&h->ctx.join[j], ev_flags);
     if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("side events", e); }
   }
-  e = hipEventCreateWithFlags(&h->ctx.fork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.classified, hipEventDisableTiming);
+  e = hipEventCreateWithFlags(&h->ctx.fork, ev_flags);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ctx.classified, ev_flags);
   if (e != hipSuccess) { cmpc_batch_destroy(h); return fail("fork event", e); }
   // the class-count hint (cmpc_launch.hip): pinned, mapped, zero (no hint) until a classify pass
   // copies a finished solve's header into it
@@ -386,8 +391,11 @@ extern "C" int cmpc_batch_enable_timing_every(cmpc_batch* h, int steps, int ever
   h->ev_solves = 0;
   for (auto e : h->ev) (void)hipEventDestroy(e);
   h->ev.assign(3 * (size_t)steps, nullptr);
+  // CMPC_EVENT_SCOPE (A/B, as the fork / join events): 2 records these timing events without the
+  // system-scope fence (a cache writeback and invalidate per record)
+  const unsigned tflags = cmpc::diag_knob("CMPC_EVENT_SCOPE", 0) == 2 ? hipEventDisableSystemFence : 0u;
   for (auto& e : h->ev)
-    if (hipError_t r = hipEventCreate(&e); r != hipSuccess) return fail("hipEventCreate", r);
+    if (hipError_t r = hipEventCreateWithFlags(&e, tflags); r != hipSuccess) return fail("hipEventCreate", r);
   h->ev_steps = steps;
   h->ev_next = 0;
   return 0;

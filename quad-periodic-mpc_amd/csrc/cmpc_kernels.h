@@ -130,7 +130,14 @@ hipError_t launch_tail(const float* d_recs, const KParams& P, float* d_forces, u
 // (the horizons without the fp64 refinement of the wide classes; with the refinement switched
 // off, cmpc_batch_set_refine(0), the longer horizons keep the 80-column class, whose parity the
 // refine-off tests cover)
-inline bool tail_class(const KParams& P, int n) { return !P.refine && P.N <= 10 && n > 64 && n <= 72; }
+__host__ __device__ inline bool tail_class(const KParams& P, int n) {
+  return !P.refine && P.N <= 10 && n > 64 && n <= 72;
+}
+// the tail class in its self-classifying form (no classify list): grid workgroups scan the batch
+// in chunks of `chunk` instances and solve its tail-class instances, launched ahead of class 1
+hipError_t launch_tail_self(const float* d_recs, int batch, const KParams& P, float* d_forces, uint8_t* d_status,
+                            int32_t* d_iters, int* ovf_list, int* ovf_count, int grid, int chunk,
+                            hipStream_t stream);
 hipError_t launch_single(const float* d_rec, int n, const KParams& P, float* d_forces,
                          uint8_t* d_status, int32_t* d_iters, const int* d_one, hipStream_t stream,
                          bool allow_tail = true);

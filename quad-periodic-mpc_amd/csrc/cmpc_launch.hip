@@ -161,9 +161,16 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   const bool wide_first = wf_env > 0 && !c1_listed && n_max > 64;
   const bool c1_list_mode = c1_listed || (wide_first && wf_env == 2);
   static const int t8_env = diag_knob("CMPC_T8_POS", -1);
-  const int t8_pos = (t8_env >= 0) ? t8_env : ((batch >= 131072 && !wide_first) ? 1 : 2);
+  // CMPC_TAIL_SELF=G (A/B, N <= 10): the tail class in its self-classifying form (no classify
+  // list) on side 2 ahead of everything, G workgroups (1: one per chunk) over chunks of
+  // CMPC_TAIL_SELF_CHUNK instances, so its long solves hold SIMD slots from the start instead of
+  // waiting for class-1 waves to retire
+  static const int tself_env = diag_knob("CMPC_TAIL_SELF", 0);
+  static const int tself_chunk = diag_knob("CMPC_TAIL_SELF_CHUNK", 64);
+  const bool tail_self = tself_env > 0 && tail_on && tself_chunk >= 1 && tself_chunk <= 64;
+  const int t8_pos = tail_self ? -1 : (t8_env >= 0) ? t8_env : ((batch >= 131072 && !wide_first) ? 1 : 2);
   // side streams forked and joined by this solve (the third only for the tail class's own chain)
-  const int nsides = (tail && t8_pos == 2) ? 3 : 2;
+  const int nsides = (tail && (t8_pos == 2 || tail_self)) ? 3 : 2;
   // CMPC_C1_SIDE=1 (A/B, N <= 10 with the tail class on side 2): class 1 and the tail class swap
   // streams — class 1 (which ends first at small batches) on side 2, the tail class on the
   // handle's stream behind the classify pass — so the join waits on queues that are already idle
@@ -178,6 +185,15 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     return launch_wide_w80(d_recs, P, d_forces, d_status, d_iters, list[10], &cnt[11], &cnt[kDeq + 10],
                            kHandoffGrid, s);
   };
+  if (tail_self) {
+    const int g = (tself_env == 1) ? (batch + tself_chunk - 1) / tself_chunk : tself_env;
+    if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess ||
+        (e = hipStreamWaitEvent(ctx.side[2], ctx.fork, 0)) != hipSuccess ||
+        (e = launch_tail_self(d_recs, batch, P, d_forces, d_status, d_iters, list[10], &cnt[11], g, tself_chunk,
+                              ctx.side[2])) != hipSuccess ||
+        (e = launch_handoff(ctx.side[2])) != hipSuccess)
+      return e;
+  }
   bool cls_side_used = false;
   int tail_grid = batch;  // the tail class's grid (hinted below when the classify pass runs)
   int tail_rest = 0;      // workgroups of its looping launch over entries past that grid
@@ -209,7 +225,7 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     if (!CMPC_HDR_MEMSET) ctx.hdr ^= 1;
     if ((e = hipEventRecord(ctx.classified, cs)) != hipSuccess) return e;
     for (int s = cls_side ? 1 : 0; s < nsides; s++)
-      if (!(c1_swap && s == 2) && (e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
+      if (!(c1_swap && s == 2) && !(tail_self && s == 2) && (e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
     if (c1_swap && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
     // launch form per wide class (cmpc_wide.h): one workgroup per entry for the class that holds
     // the trot size n = 6N, persistent workgroups (dequeue counter) for the others

@@ -1012,6 +1012,57 @@ __global__ __launch_bounds__(64, CMPC_TAIL_WAVES_PER_EU) void cmpc_solve_t_rest_
   }
 }
 
+// Self-classifying form (no classify list, so it can start ahead of class 1 instead of behind the
+// classify pass): workgroup g scans chunks g, g + G, ... of `chunk` instances, lanes < chunk count
+// the stance foot-steps of one instance each (the classify pass's test: eliminated iff
+// |gait * f_max| < 0.01, SolverMPC.cpp:869-894), and solves the chunk's tail-class instances in
+// turn with the same solve_t as the list forms (bitwise the same forces).
+__global__ __launch_bounds__(64, CMPC_TAIL_WAVES_PER_EU) void cmpc_solve_t_self_kernel(
+    const float* __restrict__ recs, int batch, KParams P, float* __restrict__ forces,
+    uint8_t* __restrict__ status, int32_t* __restrict__ iters, int* __restrict__ ovf_list,
+    int* __restrict__ ovf_count, int chunk) {
+  __shared__ SharedT<kTailRows> sh;
+#if CMPC_TAIL_PRIO > 0
+  __builtin_amdgcn_s_setprio(CMPC_TAIL_PRIO);
+#endif
+  for (int c0 = (int)blockIdx.x * chunk; c0 < batch; c0 += (int)gridDim.x * chunk) {
+    const int i = c0 + (int)threadIdx.x;
+    bool mine = false;
+    if ((int)threadIdx.x < chunk && i < batch) {
+      const uint32_t* g = reinterpret_cast<const uint32_t*>(recs + (size_t)i * P.rec_words + CMPC_REC_GAIT(P.N));
+      int nfs = 0;
+      for (int k = 0; k < P.N; k++) {
+        const uint32_t w = g[k];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const float ub = (float)((w >> (8 * j)) & 0xffu) * P.f_max;
+          nfs += (ub < 0.01f && ub > -0.01f) ? 0 : 1;
+        }
+      }
+      mine = tail_class(P, 3 * nfs);  // 64 < n <= 64 + kTailRows
+    }
+    unsigned long long m = __ballot(mine);
+    while (m) {
+      const int b = __ffsll((long long)m) - 1;
+      m &= m - 1ull;
+      const int t = c0 + b;
+      solve_t<kTailRows>(recs + (size_t)t * P.rec_words, P, sh, forces + (size_t)t * P.out_cols, status + t,
+                         iters ? iters + t : nullptr, ovf_list, ovf_count, t);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
+hipError_t launch_tail_self(const float* d_recs, int batch, const KParams& P, float* d_forces, uint8_t* d_status,
+                            int32_t* d_iters, int* ovf_list, int* ovf_count, int grid, int chunk,
+                            hipStream_t stream) {
+  if (grid <= 0 || batch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cmpc_solve_t_self_kernel, dim3(grid), dim3(64), 0, stream, d_recs, batch, P, d_forces,
+                     d_status, d_iters, ovf_list, ovf_count, chunk);
+  return hipGetLastError();
+}
+
 hipError_t launch_tail(const float* d_recs, const KParams& P, float* d_forces, uint8_t* d_status,
                        int32_t* d_iters, const int* in_list, const int* in_count, int* ovf_list,
                        int* ovf_count, int grid, hipStream_t stream, int rest_grid) {

@@ -15,7 +15,8 @@ extra=""
 for sp in "${specs[@]}"; do
   TU=${sp%%:*}; DEFS=${sp#*:}
   o=/tmp/diag_$(basename $OUT)_$TU.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 $FLAGS $DEFS -c quad-periodic-mpc_amd/csrc/$TU -o $o
+  X=""; [[ "$TU" == *.cpp ]] && X="-x hip"
+  /opt/rocm/bin/hipcc $X --offload-arch=gfx950 $FLAGS $DEFS -c quad-periodic-mpc_amd/csrc/$TU -o $o
   objs=$(echo "$objs" | grep -v "/$TU.o$")
   extra="$extra $o"
 done
