@@ -243,9 +243,15 @@ extern "C" int cmpc_batch_create(cmpc_batch** out, const cmpc_params* prm, int m
     for (int j = 0; j < cmpc::kSideStreams; j++) h->ctx.side[j] = sides[j];
     h->pooled_sides = true;
   }
-  // CMPC_EVENT_SCOPE (A/B): the fork / classified / join events' release scope: 0 the default
-  // (system scope), 1 device scope, 2 no system fence (every consumer is a queue of this device)
-  const int ev_scope = cmpc::diag_knob("CMPC_EVENT_SCOPE", 0);
+  // The fork / classified / join events order queues of this one device only: every producer and
+  // consumer of the data they guard is a kernel on this GPU, whose dispatch packets carry their own
+  // device-scope acquire / release (the per-XCD L2s written back and invalidated at kernel
+  // boundaries), and the caller's copies to the host order after the join on its stream. So these
+  // events are recorded without the system-scope fence HIP adds by default (an L2 writeback and
+  // invalidate per record, five records per solve): config 2 +3 to +4 %, 32768 instances +0.5 to
+  // +1 %, config 3 +1 % (profiles/r06_s2/env_ab.log; device scope instead: within noise).
+  // CMPC_EVENT_SCOPE (A/B): 0 HIP's default (system scope), 1 device scope, 2 no system fence
+  const int ev_scope = cmpc::diag_knob("CMPC_EVENT_SCOPE", 2);
   const unsigned ev_flags = hipEventDisableTiming | (ev_scope == 1 ? hipEventReleaseToDevice
                                                      : ev_scope == 2 ? hipEventDisableSystemFence : 0u);
   for (int j = 0; j < cmpc::kSideStreams; j++) {
@@ -391,9 +397,8 @@ extern "C" int cmpc_batch_enable_timing_every(cmpc_batch* h, int steps, int ever
   h->ev_solves = 0;
   for (auto e : h->ev) (void)hipEventDestroy(e);
   h->ev.assign(3 * (size_t)steps, nullptr);
-  // CMPC_EVENT_SCOPE (A/B, as the fork / join events): 2 records these timing events without the
-  // system-scope fence (a cache writeback and invalidate per record)
-  const unsigned tflags = cmpc::diag_knob("CMPC_EVENT_SCOPE", 0) == 2 ? hipEventDisableSystemFence : 0u;
+  // recorded without the system-scope fence too (timing only; CMPC_EVENT_SCOPE as above)
+  const unsigned tflags = cmpc::diag_knob("CMPC_EVENT_SCOPE", 2) == 2 ? hipEventDisableSystemFence : 0u;
   for (auto& e : h->ev)
     if (hipError_t r = hipEventCreateWithFlags(&e, tflags); r != hipSuccess) return fail("hipEventCreate", r);
   h->ev_steps = steps;
