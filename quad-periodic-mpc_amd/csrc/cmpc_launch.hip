@@ -24,16 +24,17 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
                                                            int* __restrict__ lists, int max_batch,
                                                            int c1_max, int* __restrict__ next_hdr,
                                                            int c1_listed, int tail,
-                                                           int* __restrict__ host_hint) {
+                                                           int* __restrict__ host_hint,
+                                                           unsigned list_mask, int header_duty) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x < kHdr) {
+  if (header_duty && blockIdx.x == 0 && threadIdx.x < kHdr) {
     // the next solve's counters: before zeroing them, the previous solve's final counts (the
     // header alternates) go to the host-mapped hint buffer (launch_solve sizes later grids by them)
     if (host_hint) host_hint[threadIdx.x] = next_hdr[threadIdx.x];
     next_hdr[threadIdx.x] = 0;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[kHdrBatch] = batch;  // this solve's batch: the hint's scale
+  if (header_duty && blockIdx.x == 0 && threadIdx.x == 0) cnt[kHdrBatch] = batch;  // this solve's batch: the hint's scale
   int cls = -1;
   if (i < batch) {
     const uint32_t* g =
@@ -60,9 +61,10 @@ __global__ __launch_bounds__(64) void cmpc_classify_kernel(const float* __restri
   const unsigned long long any = __ballot(cls >= 0);
   if (any == 0ull) return;
   const unsigned long long wide = __ballot(cls >= 0 && cls != 5);  // cnt[0]: n above class 1's build
-  if (lane == 0 && wide) atomicAdd(&cnt[0], __popcll(wide));
+  if (header_duty && lane == 0 && wide) atomicAdd(&cnt[0], __popcll(wide));
 #pragma unroll
   for (int c = 0; c < kLists; c++) {
+    if (!((list_mask >> c) & 1u)) continue;  // lists another classify launch of this solve appends
     const unsigned long long m = __ballot(cls == c);
     if (m == 0ull) continue;
     const int leader = __ffsll((long long)m) - 1;
@@ -133,7 +135,9 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
   // classify list of 60 < n <= 64 — once the batch fills the GPU (config 3: 28.4 M -> 29.3 M
   // QP/s). Below that the step is latency-bound and the extra kernel lengthens a side-stream
   // chain (config 2, batch 4096: 11.2 M -> 9.9 M), so one 64-wide launch takes all n <= 64.
-  const bool split60 = (n_max <= 64) || (batch >= 16384);
+  // CMPC_SPLIT60_MIN (A/B): the smallest batch that gets the two builds
+  static const int split_min = diag_knob("CMPC_SPLIT60_MIN", 16384);
+  const bool split60 = (n_max <= 64) || (batch >= split_min);
   const int c1_nv = (n_max <= 60 || split60) ? 60 : 64;
   // from N = 11 the trot size 6N is above class 1's rows and few instances reach class 1: it runs
   // over a classify list (list 5) instead of the whole batch (config 5: 65536 record stagings and
@@ -211,21 +215,49 @@ hipError_t launch_solve(const float* d_recs, int batch, const KParams& P, float*
     // starting without the classify pass's queue hop ahead of it pays most
     const bool cls_side = c1_swap ? true : wide_first ? false : (cls_env < 0) ? (batch >= 16384 || batch <= 4096) : (cls_env == 1);
     cls_side_used = cls_side;
-    hipStream_t cs = cls_side ? ctx.side[0] : stream;
+    // CMPC_CLS_ON_TAIL=1 (A/B): the classify pass on the tail class's own stream (side 2), so the
+    // tail class follows it in the same queue instead of after a cross-queue event (4096
+    // instances: classify ends at 16 us, the tail class started at 39 us; profiles/r06_s2)
+    static const int cls_tail_env = diag_knob("CMPC_CLS_ON_TAIL", 0);
+    const int cls_s = (cls_side && cls_tail_env == 1 && tail && t8_pos == 2 && !c1_swap) ? 2 : 0;
+    hipStream_t cs = cls_side ? ctx.side[cls_s] : stream;
     if (cls_side) {
       if ((e = hipEventRecord(ctx.fork, stream)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(ctx.side[0], ctx.fork, 0)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(ctx.side[cls_s], ctx.fork, 0)) != hipSuccess) return e;
       if (c1_swap && (e = hipStreamWaitEvent(ctx.side[2], ctx.fork, 0)) != hipSuccess) return e;
     }
+    // CMPC_CLS_PER_SIDE=1 (A/B, N <= 10, classify beside class 1, the tail class on side 2): every
+    // side stream runs its own classify pass over the lists it consumes (side 0: 80 and the 120 class
+    // when it is there; side 1: the 64-wide class-1 build, 96, 120; side 2: the tail class), so no
+    // side stream waits on another queue's event (a cross-queue event wait cost 11-21 us at 4096
+    // instances and the event between classify and the 80 class on one queue ~9 us, profiles/r06_s3)
+    static const int cps_env = diag_knob("CMPC_CLS_PER_SIDE", 0);
+    const int w120_side_c = 6 * P.N <= 80 ? 1 : 0;
+    const bool per_side = cps_env == 1 && cls_side && cls_s == 0 && tail && t8_pos == 2 && !c1_swap && !tail_self &&
+                          !c1_list_mode && n_max <= 120 && nsides == 3;
+    const unsigned all_lists = (1u << kLists) - 1u;
+    const unsigned m0 = (1u << 0) | (w120_side_c == 0 ? (1u << 8) : 0u);
+    const unsigned m1 = (1u << 1) | (1u << 7) | (w120_side_c == 1 ? (1u << 8) : 0u);
+    const unsigned m2 = (1u << 9);
+    if (per_side)
+      for (int s = 1; s < 3; s++)
+        if ((e = hipStreamWaitEvent(ctx.side[s], ctx.fork, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 63) / 64), dim3(64), 0, cs,
                        d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr, c1_list_mode ? 1 : 0,
-                       tail ? 1 : 0, ctx.d_hint);
+                       tail ? 1 : 0, ctx.d_hint, per_side ? m0 : all_lists, 1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (per_side)
+      for (int s = 1; s < 3; s++) {
+        hipLaunchKernelGGL(cmpc_classify_kernel, dim3((batch + 63) / 64), dim3(64), 0, ctx.side[s],
+                           d_recs, batch, P, cnt, d_work + 2 * kHdr, max_batch, c1_nv, next_hdr, 0,
+                           tail ? 1 : 0, nullptr, s == 1 ? m1 : m2, 0);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+      }
     ctx.last_hdr = ctx.hdr;
     if (!CMPC_HDR_MEMSET) ctx.hdr ^= 1;
-    if ((e = hipEventRecord(ctx.classified, cs)) != hipSuccess) return e;
-    for (int s = cls_side ? 1 : 0; s < nsides; s++)
-      if (!(c1_swap && s == 2) && !(tail_self && s == 2) && (e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
+    if (!per_side && (e = hipEventRecord(ctx.classified, cs)) != hipSuccess) return e;
+    for (int s = 0; s < nsides && !per_side; s++)
+      if (!(cls_side && s == cls_s) && !(c1_swap && s == 2) && !(tail_self && s == 2) && (e = hipStreamWaitEvent(ctx.side[s], ctx.classified, 0)) != hipSuccess) return e;
     if (c1_swap && (e = hipStreamWaitEvent(stream, ctx.classified, 0)) != hipSuccess) return e;
     // launch form per wide class (cmpc_wide.h): one workgroup per entry for the class that holds
     // the trot size n = 6N, persistent workgroups (dequeue counter) for the others
