@@ -15,7 +15,9 @@
 //     Cholesky columns. Because the trailing matrix of a right-looking Cholesky stays
 //     symmetric, pivot column k is "register slot[k] of every lane": ONE ds_write_b32 per step
 //     publishes it, and the broadcast reads are ds_read_b128;
-//   * J = L^-T is built column-wise from the stored L columns (lane-local updates);
+//   * J = L^-T is solved left-looking inside the factorisation's pair steps: the stored columns
+//     are -L's, lane v keeps x_j = J[v][j] in the registers of the finished H columns, and each
+//     step adds the row sums over the finished columns (16-B broadcasts, four rows per read);
 //   * the QP's triangular factor R is explicit, packed upper columns in the LDS region that held
 //     L; its back substitution and re-triangularisation are readlane chains, and the J rows see
 //     only straight-line Givens chains (identity rotations outside the active range);
@@ -52,6 +54,12 @@
 // Cholesky two pivots per step (rank-2 sweeps); 0: one pivot per step
 #ifndef CMPC_C1_CHOL2
 #define CMPC_C1_CHOL2 1
+#endif
+// J = L^-T left-looking inside the Cholesky's pair steps (no separate J pass; CMPC_C1_CHOL2 only):
+// 2 four rows per 16-B read (config 3 +2 %, 32768 instances +2 %, 4096 +1.5 %, profiles/r06_s7),
+// 1 two rows per 8-B read (-3 to -4 %), 0 the separate right-looking pass after the factorisation
+#ifndef CMPC_C1_FUSEDJ
+#define CMPC_C1_FUSEDJ 2
 #endif
 
 // Phase profiler (diagnostic builds only, -DCMPC_PHASE_PROF): lane 0 of every solved instance
@@ -394,12 +402,23 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     g0n = rl(slot[NV], j);
     g1n = fmaf(-betan, g0n, rl(slot[NV], j1));  // border of row j+1 after step j
     const float s1 = fmaf(-slot[j], betan, slot[j1]);
+#if CMPC_C1_FUSEDJ
+    // the factor's columns themselves, negated: P'_j = -L[:, j] = -slot[j] / sqrt(d_j) (and the
+    // corrected column j+1 likewise), so the sweep and the left-looking J both read them as they are
+    g0n = -g0n * i0n;
+    g1n = -g1n * i1n;
+    if (v >= cj && v < NV) sh.P[G::prow(j) + v - cj] = (v >= j) ? -slot[j] * i0n : 0.f;
+    if (v >= cj1 && v < NV) sh.P[G::prow(j1) + v - cj1] = (v >= j1) ? -s1 * i1n : 0.f;
+#else
     if (v >= cj && v < NV) sh.P[G::prow(j) + v - cj] = (v >= j) ? slot[j] : 0.f;
     if (v >= cj1 && v < NV) sh.P[G::prow(j1) + v - cj1] = (v >= j1) ? s1 : 0.f;
+#endif
     lsync();
     }
   };
   if (n > 0) look(std::integral_constant<int, 0>{});
+  float jc2 = 0.f, jc3 = 0.f;  // (CMPC_C1_FUSEDJ 2) rows k+2, k+3 of J's sums, carried one pair step
+  (void)jc2; (void)jc3;
   static_for<0, NV / 2>([&](auto KB) {
     constexpr int k = 2 * decltype(KB)::value;
     constexpr int k1 = k + 1, k2 = k + 2;
@@ -407,12 +426,22 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
     constexpr int rk = G::prow(k), rk1 = G::prow(k1);
     if (k < n) {
       const float i0 = i0n, beta = betan, i1 = i1n, g0 = g0n, g1 = g1n;
+#if CMPC_C1_FUSEDJ
+      if (v == k) my_inv = i0;
+      if (v == k1) my_inv = i1;
+      const float s0 = slot[k];
+      const float s1 = fmaf(-s0, beta, slot[k1]);
+      // row v of L in columns k, k+1 (the sweep adds l_vk P'_k + l_vk+1 P'_k+1, P' = -L)
+      const float a0 = (v > k) ? s0 * i0 : 0.f;
+      const float a1 = (v > k1) ? s1 * i1 : 0.f;
+#else
       if (v == k) { my_inv = i0; sh.u.ibuf[k] = i0; }
       if (v == k1) { my_inv = i1; sh.u.ibuf[k1] = i1; }
       const float s0 = slot[k];
       const float s1 = fmaf(-s0, beta, slot[k1]);
       const float a0 = (v > k) ? -s0 * (i0 * i0) : 0.f;
       const float a1 = (v > k1) ? -s1 * (i1 * i1) : 0.f;
+#endif
       slot[NV] = fmaf(a1, g1, fmaf(a0, g0, slot[NV]));
       static_for<c2 / 4, NV / 4>([&](auto JC) {
         constexpr int c = 4 * decltype(JC)::value;
@@ -425,6 +454,75 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         }
         CMPC_SWEEP_FENCE(c);
       });
+#if CMPC_C1_FUSEDJ == 2
+      // J = L^-T, left-looking, four rows per 16-B read: at k = 0 mod 4 the sums of rows k..k+3
+      // over every finished column j < k (one ds_read_b128 broadcast of P'_j[k..k+3] per column,
+      // loads of the next group issued before the FMAs of this one, two accumulators per row);
+      // rows k, k+1 are finished here, rows k+2, k+3 carry to the next pair step, which adds the
+      // terms of columns k, k+1 (two 8-B reads)
+      if constexpr ((k & 3) == 0) {
+        f2v t0 = {(v == k) ? 1.f : 0.f, 0.f}, t1 = {(v == k1) ? 1.f : 0.f, 0.f};
+        f2v t2 = {(v == k + 2) ? 1.f : 0.f, 0.f}, t3 = {(v == k + 3) ? 1.f : 0.f, 0.f};
+        static_for<0, k / 4>([&](auto QC) {
+          constexpr int q = 4 * decltype(QC)::value;  // columns q .. q+3 (4 | k)
+          const float4 la = *reinterpret_cast<const float4*>(&sh.P[G::prow(q) + k - q]);
+          const float4 lb = *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 1) + k - q]);
+          const float4 lc = *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 2) + k - q]);
+          const float4 ld = *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 3) + k - q]);
+          t0.x = fmaf(slot[q], la.x, t0.x); t1.x = fmaf(slot[q], la.y, t1.x);
+          t2.x = fmaf(slot[q], la.z, t2.x); t3.x = fmaf(slot[q], la.w, t3.x);
+          t0.y = fmaf(slot[q + 1], lb.x, t0.y); t1.y = fmaf(slot[q + 1], lb.y, t1.y);
+          t2.y = fmaf(slot[q + 1], lb.z, t2.y); t3.y = fmaf(slot[q + 1], lb.w, t3.y);
+          t0.x = fmaf(slot[q + 2], lc.x, t0.x); t1.x = fmaf(slot[q + 2], lc.y, t1.x);
+          t2.x = fmaf(slot[q + 2], lc.z, t2.x); t3.x = fmaf(slot[q + 2], lc.w, t3.x);
+          t0.y = fmaf(slot[q + 3], ld.x, t0.y); t1.y = fmaf(slot[q + 3], ld.y, t1.y);
+          t2.y = fmaf(slot[q + 3], ld.z, t2.y); t3.y = fmaf(slot[q + 3], ld.w, t3.y);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        const float hk = sh.P[G::prow(k) + k1 - (k & ~3)];  // -L[k+1][k]
+        const float xk = (t0.x + t0.y) * i0;
+        slot[k] = xk;
+        slot[k1] = fmaf(xk, hk, t1.x + t1.y) * i1;
+        jc2 = t2.x + t2.y;
+        jc3 = t3.x + t3.y;
+        asm volatile("" : "+v"(jc2), "+v"(jc3));
+      } else {
+        constexpr int km = k - 2;  // the columns of the pair step before (k - 2 = 0 mod 4)
+        const float2 l0 = *reinterpret_cast<const float2*>(&sh.P[G::prow(km) + k - (km & ~3)]);
+        const float2 l1 = *reinterpret_cast<const float2*>(&sh.P[G::prow(km + 1) + k - (km & ~3)]);
+        const float hk = sh.P[G::prow(k) + k1 - (k & ~3)];
+        const float e0 = fmaf(slot[km + 1], l1.x, fmaf(slot[km], l0.x, jc2));
+        const float e1 = fmaf(slot[km + 1], l1.y, fmaf(slot[km], l0.y, jc3));
+        const float xk = e0 * i0;
+        slot[k] = xk;
+        slot[k1] = fmaf(xk, hk, e1) * i1;
+      }
+#elif CMPC_C1_FUSEDJ
+      // J = L^-T, left-looking: lane v solves L x = e_v, x_k = (d_vk - sum_{j<k} L[k][j] x_j) / L[k][k];
+      // x_j (j < k) sit in the registers of the factor's finished columns, L[k][j], L[k+1][j] are
+      // one 8-B broadcast of the stored column j (k even, rows start 16-B aligned), two interleaved
+      // accumulators per row keep the FMA chains short. Every column of the factor is thus read
+      // once more here instead of in a separate pass of 30 serial steps after the factorisation.
+      {
+        float e0 = (v == k) ? 1.f : 0.f, e1 = (v == k1) ? 1.f : 0.f, o0 = 0.f, o1 = 0.f;
+        static_for<0, k>([&](auto JJ) {
+          constexpr int j = decltype(JJ)::value;
+          const float2 lj = *reinterpret_cast<const float2*>(&sh.P[G::prow(j) + k - (j & ~3)]);
+          if constexpr ((j & 1) == 0) {
+            e0 = fmaf(slot[j], lj.x, e0);
+            e1 = fmaf(slot[j], lj.y, e1);
+          } else {
+            o0 = fmaf(slot[j], lj.x, o0);
+            o1 = fmaf(slot[j], lj.y, o1);
+          }
+          if constexpr ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        });
+        const float hk = sh.P[G::prow(k) + k1 - (k & ~3)];  // -L[k+1][k]
+        const float xk = (e0 + o0) * i0;
+        slot[k] = xk;
+        slot[k1] = fmaf(xk, hk, e1 + o1) * i1;
+      }
+#endif
       pin(slot);
     }
   });
@@ -490,11 +588,16 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   C1_MARK(2);
 
   // ---- J = L^-T: lane v solves L x = e_v (column v of L^-1 = row v of J) -----------------
+#if CMPC_C1_CHOL2 && CMPC_C1_FUSEDJ
+  // done inside the factorisation above; the columns past n are the identity rows' e_v already
+#else
   static_for<0, NV>([&](auto C) {
     constexpr int c = decltype(C)::value;
     slot[c] = (c == v) ? 1.f : 0.f;
   });
-#if CMPC_C1_CHOL2
+#endif
+#if CMPC_C1_CHOL2 && CMPC_C1_FUSEDJ
+#elif CMPC_C1_CHOL2
   // two columns per step, as the factorisation: x_k, then x_k+1 after column k's term, then one
   // rank-2 sweep over the stored columns k, k+1 (the odd-n padding column is the identity)
   static_for<0, NV / 2>([&](auto KB) {

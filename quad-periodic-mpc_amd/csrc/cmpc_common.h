@@ -177,6 +177,9 @@ __device__ __forceinline__ void piped_sweep(Ld&& ld, F&& f) {
 struct F4x2 {
   float4 a, b;
 };
+struct F4x4 {
+  float4 a, b, c, d;
+};
 
 // An SGPR value the compiler cannot see through: keeps per-iteration scalar work of an unrolled
 // loop inside its iteration (otherwise LICM hoists dozens of SGPRs out of it -> spills).
