@@ -61,6 +61,10 @@
 #ifndef CMPC_C1_FUSEDJ
 #define CMPC_C1_FUSEDJ 2
 #endif
+// (form 2) the J row sums' column loads software-pipelined one group ahead (A/B)
+#ifndef CMPC_C1_JPIPE
+#define CMPC_C1_JPIPE 0
+#endif
 
 // Phase profiler (diagnostic builds only, -DCMPC_PHASE_PROF): lane 0 of every solved instance
 // adds the s_memtime cycles spent in each stage to g_c1_phase (scripts/phase_prof.py).
@@ -457,18 +461,33 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 #if CMPC_C1_FUSEDJ == 2
       // J = L^-T, left-looking, four rows per 16-B read: at k = 0 mod 4 the sums of rows k..k+3
       // over every finished column j < k (one ds_read_b128 broadcast of P'_j[k..k+3] per column,
-      // loads of the next group issued before the FMAs of this one, two accumulators per row);
+      // four columns per scheduling group, two accumulators per row);
       // rows k, k+1 are finished here, rows k+2, k+3 carry to the next pair step, which adds the
       // terms of columns k, k+1 (two 8-B reads)
       if constexpr ((k & 3) == 0) {
         f2v t0 = {(v == k) ? 1.f : 0.f, 0.f}, t1 = {(v == k1) ? 1.f : 0.f, 0.f};
         f2v t2 = {(v == k + 2) ? 1.f : 0.f, 0.f}, t3 = {(v == k + 3) ? 1.f : 0.f, 0.f};
+#if CMPC_C1_JPIPE
+        // loads of the next column group issued before this group's FMAs (one group ahead)
+        piped_sweep<0, k, 1>(
+            [&](auto C) {
+              constexpr int q = decltype(C)::value;  // columns q .. q+3 (4 | k)
+              return F4x4{*reinterpret_cast<const float4*>(&sh.P[G::prow(q) + k - q]),
+                          *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 1) + k - q]),
+                          *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 2) + k - q]),
+                          *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 3) + k - q])};
+            },
+            [&](auto C, F4x4 l) {
+              constexpr int q = decltype(C)::value;
+              const float4 la = l.a, lb = l.b, lc = l.c, ld = l.d;
+#else
         static_for<0, k / 4>([&](auto QC) {
           constexpr int q = 4 * decltype(QC)::value;  // columns q .. q+3 (4 | k)
           const float4 la = *reinterpret_cast<const float4*>(&sh.P[G::prow(q) + k - q]);
           const float4 lb = *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 1) + k - q]);
           const float4 lc = *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 2) + k - q]);
           const float4 ld = *reinterpret_cast<const float4*>(&sh.P[G::prow(q + 3) + k - q]);
+#endif
           t0.x = fmaf(slot[q], la.x, t0.x); t1.x = fmaf(slot[q], la.y, t1.x);
           t2.x = fmaf(slot[q], la.z, t2.x); t3.x = fmaf(slot[q], la.w, t3.x);
           t0.y = fmaf(slot[q + 1], lb.x, t0.y); t1.y = fmaf(slot[q + 1], lb.y, t1.y);
@@ -477,8 +496,12 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           t2.x = fmaf(slot[q + 2], lc.z, t2.x); t3.x = fmaf(slot[q + 2], lc.w, t3.x);
           t0.y = fmaf(slot[q + 3], ld.x, t0.y); t1.y = fmaf(slot[q + 3], ld.y, t1.y);
           t2.y = fmaf(slot[q + 3], ld.z, t2.y); t3.y = fmaf(slot[q + 3], ld.w, t3.y);
+#if CMPC_C1_JPIPE
+            });
+#else
           __builtin_amdgcn_sched_barrier(0);
         });
+#endif
         const float hk = sh.P[G::prow(k) + k1 - (k & ~3)];  // -L[k+1][k]
         const float xk = (t0.x + t0.y) * i0;
         slot[k] = xk;
