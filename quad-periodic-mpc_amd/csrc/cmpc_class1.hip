@@ -61,9 +61,10 @@
 #ifndef CMPC_C1_FUSEDJ
 #define CMPC_C1_FUSEDJ 2
 #endif
-// (form 2) the J row sums' column loads software-pipelined one group ahead (A/B)
+// (form 2) the J row sums' column loads software-pipelined one group ahead: config 3 +0.9 /
+// +1.3 %, 4096 +0.6 / +0.8 %, 32768 -0.2 % (profiles/r06_s9/lib_ab.log); 0: one group at a time
 #ifndef CMPC_C1_JPIPE
-#define CMPC_C1_JPIPE 0
+#define CMPC_C1_JPIPE 1
 #endif
 
 // Phase profiler (diagnostic builds only, -DCMPC_PHASE_PROF): lane 0 of every solved instance
@@ -461,7 +462,8 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 #if CMPC_C1_FUSEDJ == 2
       // J = L^-T, left-looking, four rows per 16-B read: at k = 0 mod 4 the sums of rows k..k+3
       // over every finished column j < k (one ds_read_b128 broadcast of P'_j[k..k+3] per column,
-      // four columns per scheduling group, two accumulators per row);
+      // four columns per group, the next group's loads issued before this group's FMAs, two
+      // accumulators per row);
       // rows k, k+1 are finished here, rows k+2, k+3 carry to the next pair step, which adds the
       // terms of columns k, k+1 (two 8-B reads)
       if constexpr ((k & 3) == 0) {
