@@ -66,6 +66,12 @@
 #ifndef CMPC_C1_JPIPE
 #define CMPC_C1_JPIPE 1
 #endif
+// (form 2) x = -J y accumulated inside the factorisation (two FMAs per pair step with the
+// step's border values) instead of an LDS sweep after it: config 3 +0.8 / +1.8 %, 4096 +0.3 /
+// +0.9 %, 32768 -0.4 / +1.4 % (profiles/r06_s12/lib_ab.log)
+#ifndef CMPC_C1_XUNC
+#define CMPC_C1_XUNC 1
+#endif
 
 // Phase profiler (diagnostic builds only, -DCMPC_PHASE_PROF): lane 0 of every solved instance
 // adds the s_memtime cycles spent in each stage to g_c1_phase (scripts/phase_prof.py).
@@ -424,6 +430,10 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
   if (n > 0) look(std::integral_constant<int, 0>{});
   float jc2 = 0.f, jc3 = 0.f;  // (CMPC_C1_FUSEDJ 2) rows k+2, k+3 of J's sums, carried one pair step
   (void)jc2; (void)jc3;
+  // (CMPC_C1_XUNC) x = -J y accumulated as J's entries are solved: y_k = -g0 of pair step k (the
+  // border of row k after the pivots before it, scaled by -1/sqrt(d_k) in look)
+  float xunc = 0.f;
+  (void)xunc;
   static_for<0, NV / 2>([&](auto KB) {
     constexpr int k = 2 * decltype(KB)::value;
     constexpr int k1 = k + 1, k2 = k + 2;
@@ -508,6 +518,9 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         const float xk = (t0.x + t0.y) * i0;
         slot[k] = xk;
         slot[k1] = fmaf(xk, hk, t1.x + t1.y) * i1;
+#if CMPC_C1_XUNC
+        xunc = fmaf(slot[k1], g1, fmaf(xk, g0, xunc));
+#endif
         jc2 = t2.x + t2.y;
         jc3 = t3.x + t3.y;
         asm volatile("" : "+v"(jc2), "+v"(jc3));
@@ -521,6 +534,9 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
         const float xk = e0 * i0;
         slot[k] = xk;
         slot[k1] = fmaf(xk, hk, e1) * i1;
+#if CMPC_C1_XUNC
+        xunc = fmaf(slot[k1], g1, fmaf(xk, g0, xunc));
+#endif
       }
 #elif CMPC_C1_FUSEDJ
       // J = L^-T, left-looking: lane v solves L x = e_v, x_k = (d_vk - sum_{j<k} L[k][j] x_j) / L[k][k];
@@ -672,6 +688,10 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
 
   C1_MARK(3);
   // ---- unconstrained minimiser x = -J y ----------------------------------------------------
+#if CMPC_C1_FUSEDJ == 2 && CMPC_C1_XUNC
+  (void)yv;
+  float xv = (v < n) ? xunc : 0.f;  // accumulated in the factorisation's steps
+#else
   sh.vbuf()[v] = yv;
   lsync();
   f2v xacc = {0.f, 0.f};
@@ -683,6 +703,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
       });
   float xv = (v < n) ? -(xacc.x + xacc.y) : 0.f;
   lsync();
+#endif
 
   // ---- Goldfarb-Idnani dual active set on the friction pyramids -----------------------------
   // One flat loop, one active-set step per trip. The QP's triangular factor R (q x q) is kept
