@@ -66,6 +66,16 @@
 #ifndef CMPC_C1_JPIPE
 #define CMPC_C1_JPIPE 1
 #endif
+// the active set's row-long dot products (z = J2 d2, |d2|^2, J_v . w) as two interleaved FMA
+// chains (dot4x2) instead of one (A/B)
+#ifndef CMPC_C1_DOT2
+#define CMPC_C1_DOT2 0
+#endif
+#if CMPC_C1_DOT2
+#define C1_DOT dot4x2
+#else
+#define C1_DOT dot4
+#endif
 // (form 2) x = -J y accumulated inside the factorisation (two FMAs per pair step with the
 // step's border values) instead of an LDS sweep after it: config 3 +0.8 / +1.8 %, 4096 +0.3 /
 // +0.9 %, 32768 -0.4 / +1.4 % (profiles/r06_s12/lib_ab.log)
@@ -786,8 +796,8 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
           [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf()[decltype(C)::value]); },
           [&](auto C, float4 m4) {
             constexpr int c = decltype(C)::value;
-            dot4(zacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], m4);
-            dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
+            C1_DOT(zacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], m4);
+            C1_DOT(nacc, m4.x, m4.y, m4.z, m4.w, m4);
           });
       float zv = zacc.x + zacc.y, zn = nacc.x + nacc.y;
       // materialise both sums here: otherwise the FMAs sink below the back substitution loop
@@ -952,7 +962,7 @@ __device__ __forceinline__ void solve_c1(const float* __restrict__ rec, const KP
             [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf()[decltype(C)::value]); },
             [&](auto C, float4 w4) {
               constexpr int c = decltype(C)::value;
-              dot4(tacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], w4);
+              C1_DOT(tacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], w4);
             });
         const float bt = -beta * (tacc.x + tacc.y);
         // re-read w from LDS: without this point the compiler keeps all NV values of the first

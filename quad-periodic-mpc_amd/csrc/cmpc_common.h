@@ -220,6 +220,14 @@ __device__ __forceinline__ void dot4(f2v& acc, float x0, float x1, float x2, flo
   acc.x = fmaf(x2, r.z, acc.x);
   acc.x = fmaf(x3, r.w, acc.x);
 }
+// the same with two interleaved chains (acc.x: even columns, acc.y: odd): half the dependent FMA
+// latency of a row-long dot product
+__device__ __forceinline__ void dot4x2(f2v& acc, float x0, float x1, float x2, float x3, float4 r) {
+  acc.x = fmaf(x0, r.x, acc.x);
+  acc.y = fmaf(x1, r.y, acc.y);
+  acc.x = fmaf(x2, r.z, acc.x);
+  acc.y = fmaf(x3, r.w, acc.y);
+}
 
 // single-wavefront workgroup: orders this wave's LDS traffic without an s_barrier
 __device__ __forceinline__ void wsync() {

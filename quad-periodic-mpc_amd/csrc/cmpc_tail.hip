@@ -35,6 +35,15 @@
 #ifndef CMPC_TAIL_TRIP_PRIO
 #define CMPC_TAIL_TRIP_PRIO 3
 #endif
+// the active set's row-long dot products as two interleaved FMA chains (A/B)
+#ifndef CMPC_TAIL_DOT2
+#define CMPC_TAIL_DOT2 0
+#endif
+#if CMPC_TAIL_DOT2
+#define T_DOT dot4x2
+#else
+#define T_DOT dot4
+#endif
 #ifndef CMPC_TAIL_PRIO  // s_setprio of the tail classes' waves: issue ahead of the class-1 waves on their SIMDs
 #define CMPC_TAIL_PRIO 1
 #endif
@@ -720,8 +729,8 @@ __device__ __forceinline__ void solve_t(const float* __restrict__ rec, const KPa
           [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf()[decltype(C)::value]); },
           [&](auto C, float4 m4) {
             constexpr int c = decltype(C)::value;
-            dot4(zacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], m4);
-            dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
+            T_DOT(zacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], m4);
+            T_DOT(nacc, m4.x, m4.y, m4.z, m4.w, m4);
           });
       float zv = zacc.x + zacc.y, zn = nacc.x + nacc.y;
       float zt;
@@ -875,7 +884,7 @@ __device__ __forceinline__ void solve_t(const float* __restrict__ rec, const KPa
             [&](auto C) { return *reinterpret_cast<const float4*>(&sh.vbuf()[decltype(C)::value]); },
             [&](auto C, float4 w4) {
               constexpr int c = decltype(C)::value;
-              dot4(tacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], w4);
+              T_DOT(tacc, slot[c + 0], slot[c + 1], slot[c + 2], slot[c + 3], w4);
             });
         const float bt = -beta * (tacc.x + tacc.y);
         float ta = 0.f;

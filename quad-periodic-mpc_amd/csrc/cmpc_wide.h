@@ -61,6 +61,15 @@
 #ifndef CMPC_WIDE_TRIP_PRIO
 #define CMPC_WIDE_TRIP_PRIO 3
 #endif
+// the active set's half-row dot products (z, |d2|^2, J_r . w) as two interleaved FMA chains (A/B)
+#ifndef CMPC_WIDE_DOT2
+#define CMPC_WIDE_DOT2 0
+#endif
+#if CMPC_WIDE_DOT2
+#define W_DOT dot4x2
+#else
+#define W_DOT dot4
+#endif
 #ifndef CMPC_WIDE_PRIO  // s_setprio of the wide classes' waves (0: the default priority)
 #define CMPC_WIDE_PRIO 0
 #endif
@@ -1100,8 +1109,8 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
 #pragma unroll
         for (int j = 0; j < NH; j += 4) {
           const float4 m4 = *reinterpret_cast<const float4*>(vb + j);
-          dot4(zacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], m4);
-          dot4(nacc, m4.x, m4.y, m4.z, m4.w, m4);
+          W_DOT(zacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], m4);
+          W_DOT(nacc, m4.x, m4.y, m4.z, m4.w, m4);
           CMPC_WGI_FENCE(j);
         }
         zv = pair_sum(zacc.x + zacc.y);
@@ -1371,7 +1380,7 @@ __device__ __forceinline__ void solve_w(const float* __restrict__ rec, const KPa
 #pragma unroll
         for (int j = 0; j < NH; j += 4) {
           const float4 w4 = *reinterpret_cast<const float4*>(vb + j);
-          dot4(tacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], w4);
+          W_DOT(tacc, slot[j + 0], slot[j + 1], slot[j + 2], slot[j + 3], w4);
           CMPC_WGI_FENCE(j);
         }
         const float bt = -beta * pair_sum(tacc.x + tacc.y);
